@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""bench.py -- FA2 forward+backward on MI355X, BASELINE.json's headline metric.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c5|c1]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+One *step* = the FA2 forward (O, LSE) + backward (Δ, dK/dV, dQ) over one batch
+of synthetic fp32 inputs already resident in HBM (harness distribution:
+torch.manual_seed(42 + rank), torch.rand for Q, K, V; dO = ones as the reference
+harness uses, test_flash_attention2.py:220-232).  Default workload is BASELINE
+config C3, B4_H16_S2048_D64, fp16 tiles on MFMA -- the config the metric is
+quoted on ("... at S=2048 D=64"), per rank: multi-GPU runs shard batch x heads,
+each rank owning its own B*H slice with no data-path collective
+(scaling "weak"; --workload c5 instead splits B64_H16_S2048_D64 over the ranks).
+
+value = algorithmic fwd+bwd FLOPs of all ranks (14*B*H*S^2*D each) / the max over
+ranks of the K-step wall time (barrier + synchronize on both sides).
+roofline = the dominant kernel's algorithmic FLOPs / its mean duration, timed
+live with HIP events recorded on the kernel's own stream around every launch of
+the timed region, against the dense fp16 MFMA peak.  cpu_baseline = the C
+restatement of the oracle (oracle/fa2_oracle.c, "port") on the host cores, on a
+bounded sample of the same workload (whole heads, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cuda-flash-attention_amd"))
+
+MFMA_F16_PEAK_TFLOPS = 2500.0   # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFLOPS = 157.3    # fp32 MFMA = fp32 vector peak
+HBM_PEAK_GBPS = 8000.0
+
+WORKLOADS = {
+    # name: (B, H, S, D, per_rank)
+    "c3": (4, 16, 2048, 64, True),
+    "c5": (64, 16, 2048, 64, False),
+    "c1": (2, 8, 512, 64, True),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def traffic_from_profile(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_summary.json, written by tools/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            ent = json.load(f).get(kernel)
+        return None if ent is None else float(ent["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def cpu_baseline(S, D, sample_heads=None):
+    """Time the C oracle (fwd + bwd) on whole heads of the workload's shape."""
+    from oracle import c_oracle, fa2_oracle as fo
+
+    cores = len(os.sched_getaffinity(0))
+    threads = max(1, min(cores, 16))
+    heads = sample_heads or threads
+    q, k, v = fo.harness_inputs(1, heads, S, D, seed=42)
+    do = np.ones_like(q)
+    c_oracle.forward(q[:, :1, :64], k[:, :1, :64], v[:, :1, :64], 1)  # load/build outside the timed region
+    t0 = time.perf_counter()
+    o, lse = c_oracle.forward(q, k, v, nthreads=threads)
+    c_oracle.backward(q, k, v, o, do, lse, nthreads=threads)
+    dt = time.perf_counter() - t0
+    flops = 14.0 * heads * S * S * D
+    return {"value": round(flops / dt / 1e12, 5), "unit": "TFLOPS", "cores": threads, "kind": "port",
+            "sample": f"{heads} heads x (S={S}, D={D}) fp32 fwd+bwd, oracle/fa2_oracle.c, {dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--precision", choices=["fp16", "fp32"], default="fp16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import fa2amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    B, H, S, D, per_rank = WORKLOADS[args.workload]
+    if per_rank:
+        heads = B * H
+        Bl, Hl = B, H
+    else:
+        first, heads = fa2amd.shard_range(B * H, world, rank)
+        Bl, Hl = 1, heads
+
+    gen = torch.Generator().manual_seed(42 + rank)
+    q = torch.rand(Bl, Hl, S, D, generator=gen).to(dev)
+    k = torch.rand(Bl, Hl, S, D, generator=gen).to(dev)
+    v = torch.rand(Bl, Hl, S, D, generator=gen).to(dev)
+    do = torch.ones_like(q)
+    o = torch.empty_like(q)
+    lse = torch.empty(Bl, Hl, S, device=dev)
+    dl = torch.empty(Bl, Hl, S, device=dev)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
+    stream = torch.cuda.current_stream(dev)
+    prec = args.precision
+
+    kernels = ["fwd", "delta", "dkdv", "dq"] if prec == "fp16" else ["fwd", "bwd"]
+
+    def step(ev=None):
+        def mark(i):
+            if ev is not None:
+                ev[i].record(stream)
+        mark(0)
+        fa2amd.forward(q, k, v, prec, out=o, lse=lse, stream=stream)
+        mark(1)
+        if prec == "fp16":
+            fa2amd.delta(do, o, out=dl, stream=stream)
+            mark(2)
+            fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv, stream=stream)
+            mark(3)
+            fa2amd.backward_dq(q, k, v, do, lse, dl, dq, stream=stream)
+            mark(4)
+        else:
+            fa2amd.backward(q, k, v, o, do, lse, prec, dq=dq, dk=dk, dv=dv, delta_buf=dl, stream=stream)
+            mark(2)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    nev = len(kernels) + 1
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(nev)] for _ in range(args.steps)]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(events[s])
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel mean durations (ms) over the timed region
+    kms = {name: float(np.mean([events[s][i].elapsed_time(events[s][i + 1]) for s in range(args.steps)]))
+           for i, name in enumerate(kernels)}
+
+    per_head = S * S * D
+    total_heads = B * H * world if per_rank else B * H
+    flops = 14.0 * per_head * total_heads * args.steps
+    tflops = flops / elapsed / 1e12
+    hbm_bytes = (48.0 * S * D + 8.0 * S) * total_heads * args.steps  # fwd 16SD+4S, bwd 32SD+4S per head
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # dominant kernel and its algorithmic FLOPs per launch
+    alg = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "delta": 0.0, "bwd": 10.0}
+    dom = max(kms, key=kms.get)
+    dom_flops = alg[dom] * per_head * heads
+    peak = MFMA_F16_PEAK_TFLOPS if prec == "fp16" else MFMA_F32_PEAK_TFLOPS
+    achieved = dom_flops / (kms[dom] * 1e-3) / 1e12
+    roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic_from_profile(dom),
+            "kernel_ms": {n: round(x, 4) for n, x in kms.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(S, D)
+        except Exception as e:  # the baseline is reported, never required
+            log("cpu baseline failed:", e)
+
+    if rank == 0:
+        line = {
+            "metric": "FA2 fwd+bwd TFLOPS & HBM GB/s (% of gfx950 roofline) at S=2048 D=64",
+            "value": round(tflops, 3),
+            "unit": "TFLOPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if per_rank else "strong",
+            "vs_baseline": None,
+            "dtype": prec,
+            "data": "synthetic (torch.rand U[0,1) Q/K/V as the reference harness draws them, dO = ones)",
+            "config": {"workload": f"B{B}_H{H}_S{S}_D{D} {prec}-tile fwd+bwd" + (" per rank" if per_rank else ""),
+                       "batch": B, "heads": H, "seq_len": S, "head_dim": D,
+                       "parallelism": f"bh-shard{world}" if world > 1 else "single"},
+            "hbm_gbps": round(hbm_bytes / elapsed / 1e9, 2),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

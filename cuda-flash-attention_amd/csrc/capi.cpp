@@ -1,0 +1,276 @@
+// capi.cpp -- implementation of include/fa2_amd.h on top of the launch layer
+// (namespace fa2, declared in kernels/f-attn2.cuh).
+#include "fa2_amd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "f-attn2.cuh"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int check_shape(int B, int H, int S, int D) {
+    if (B <= 0 || H <= 0 || S <= 0) return fail(FA2_E_INVALID, "batch, heads and seq must be positive");
+    if (!fa2::supported_head_dim(D)) return fail(FA2_E_INVALID, "head_dim must be 32, 64 or 128");
+    if ((long long)B * H * S * D > 0x7fffffffLL * 4)
+        return fail(FA2_E_INVALID, "tensor too large (B*H*S*D must fit the 32-bit launch grid)");
+    if ((long long)B * H > 0x7fffffffLL / ((S + 31) / 32)) return fail(FA2_E_INVALID, "grid too large");
+    return FA2_OK;
+}
+
+int check_ptrs(std::initializer_list<const void*> ps) {
+    for (const void* p : ps)
+        if (!p) return fail(FA2_E_INVALID, "null tensor pointer");
+    return FA2_OK;
+}
+
+int hip_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return FA2_OK;
+    return fail(e == hipErrorOutOfMemory ? FA2_E_NOMEM : FA2_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int check_precision(int precision) {
+    if (precision != FA2_FP16 && precision != FA2_FP32) return fail(FA2_E_INVALID, "precision must be FA2_FP16 or FA2_FP32");
+    return FA2_OK;
+}
+
+// RAII device buffer
+struct DevBuf {
+    float* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int fa2_version(void) { return 1 * 10000 + 0 * 100 + 0; }
+
+const char* fa2_last_error(void) { return g_err.c_str(); }
+
+int fa2_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int fa2_shard_range(int total_heads, int shards, int index, int* first, int* count) {
+    if (total_heads < 0 || shards <= 0 || index < 0 || index >= shards || !first || !count)
+        return fail(FA2_E_INVALID, "bad shard arguments");
+    const int q = total_heads / shards, r = total_heads % shards;
+    *first = index * q + std::min(index, r);
+    *count = q + (index < r ? 1 : 0);
+    return FA2_OK;
+}
+
+int fa2_forward(const float* q, const float* k, const float* v, float* o, float* lse, int B, int H, int S, int D,
+                int precision, void* stream) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_precision(precision)) || (rc = check_ptrs({q, k, v, o, lse})))
+        return rc;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const hipError_t e = precision == FA2_FP16 ? fa2::launch_forward_f16(D, q, k, v, o, lse, B * H, S, st)
+                                               : fa2::launch_forward_f32(D, q, k, v, o, lse, B * H, S, st);
+    return hip_status(e, "fa2_forward launch");
+}
+
+int fa2_delta(const float* dout, const float* o, float* delta, int B, int H, int S, int D, void* stream) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_ptrs({dout, o, delta}))) return rc;
+    return hip_status(fa2::launch_delta(D, dout, o, delta, B * H, S, static_cast<hipStream_t>(stream)),
+                      "fa2_delta launch");
+}
+
+int fa2_backward(const float* q, const float* k, const float* v, const float* o, const float* dout, const float* lse,
+                 float* delta, float* dq, float* dk, float* dv, int B, int H, int S, int D, int precision,
+                 void* stream) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_precision(precision)) ||
+        (rc = check_ptrs({q, k, v, o, dout, lse, delta, dq, dk, dv})))
+        return rc;
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    const hipError_t e =
+        precision == FA2_FP16 ? fa2::launch_backward_f16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st)
+                              : fa2::launch_backward_f32(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st);
+    return hip_status(e, "fa2_backward launch");
+}
+
+int fa2_backward_dkdv(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                      const float* delta, float* dk, float* dv, int B, int H, int S, int D, void* stream) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_ptrs({q, k, v, dout, lse, delta, dk, dv}))) return rc;
+    return hip_status(
+        fa2::launch_bwd_dkdv_f16(D, q, k, v, dout, lse, delta, dk, dv, B * H, S, static_cast<hipStream_t>(stream)),
+        "fa2_backward_dkdv launch");
+}
+
+int fa2_backward_dq(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                    const float* delta, float* dq, int B, int H, int S, int D, void* stream) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_ptrs({q, k, v, dout, lse, delta, dq}))) return rc;
+    return hip_status(
+        fa2::launch_bwd_dq_f16(D, q, k, v, dout, lse, delta, dq, B * H, S, static_cast<hipStream_t>(stream)),
+        "fa2_backward_dq launch");
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// host-pointer API (+ B*H sharding over devices)
+// ---------------------------------------------------------------------------
+namespace {
+
+struct HostJob {
+    // host tensors (full) and this shard's head range
+    const float* in[6] = {};  // q k v o dout lse
+    float* out[5] = {};       // o lse | dq dk dv
+    int heads0 = 0, nheads = 0, S = 0, D = 0, precision = 0, device = 0;
+    bool backward = false;
+    float ms = 0.f;
+    int rc = FA2_OK;
+    std::string err;
+};
+
+int run_shard(HostJob& j) {
+    const size_t row = (size_t)j.S * j.D;             // floats per head, [S][D]
+    const size_t n = (size_t)j.nheads * row;          // floats per tensor in this shard
+    const size_t nl = (size_t)j.nheads * j.S;         // floats per [heads][S] vector
+    const size_t off = (size_t)j.heads0 * row, offl = (size_t)j.heads0 * j.S;
+    if (hipSetDevice(j.device) != hipSuccess) return fail(FA2_E_DEVICE, "hipSetDevice failed");
+    int rc;
+    hipStream_t st = nullptr;
+    if ((rc = hip_status(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
+    struct StreamGuard {
+        hipStream_t s;
+        ~StreamGuard() { (void)hipStreamDestroy(s); }
+    } sg{st};
+    hipEvent_t e0, e1;
+    if ((rc = hip_status(hipEventCreate(&e0), "hipEventCreate"))) return rc;
+    if ((rc = hip_status(hipEventCreate(&e1), "hipEventCreate"))) {
+        (void)hipEventDestroy(e0);
+        return rc;
+    }
+    struct EventGuard {
+        hipEvent_t a, b;
+        ~EventGuard() {
+            (void)hipEventDestroy(a);
+            (void)hipEventDestroy(b);
+        }
+    } eg{e0, e1};
+
+    if (!j.backward) {
+        DevBuf q, k, v, o, l;
+        if ((rc = hip_status(hipMalloc(&q.p, n * 4), "hipMalloc")) || (rc = hip_status(hipMalloc(&k.p, n * 4), "hipMalloc")) ||
+            (rc = hip_status(hipMalloc(&v.p, n * 4), "hipMalloc")) || (rc = hip_status(hipMalloc(&o.p, n * 4), "hipMalloc")) ||
+            (rc = hip_status(hipMalloc(&l.p, nl * 4), "hipMalloc")))
+            return rc;
+        if ((rc = hip_status(hipMemcpy(q.p, j.in[0] + off, n * 4, hipMemcpyHostToDevice), "H2D")) ||
+            (rc = hip_status(hipMemcpy(k.p, j.in[1] + off, n * 4, hipMemcpyHostToDevice), "H2D")) ||
+            (rc = hip_status(hipMemcpy(v.p, j.in[2] + off, n * 4, hipMemcpyHostToDevice), "H2D")))
+            return rc;
+        (void)hipEventRecord(e0, st);
+        rc = fa2_forward(q.p, k.p, v.p, o.p, l.p, 1, j.nheads, j.S, j.D, j.precision, st);
+        if (rc) return rc;
+        (void)hipEventRecord(e1, st);
+        if ((rc = hip_status(hipEventSynchronize(e1), "kernel"))) return rc;
+        (void)hipEventElapsedTime(&j.ms, e0, e1);
+        if ((rc = hip_status(hipMemcpy(j.out[0] + off, o.p, n * 4, hipMemcpyDeviceToHost), "D2H")) ||
+            (rc = hip_status(hipMemcpy(j.out[1] + offl, l.p, nl * 4, hipMemcpyDeviceToHost), "D2H")))
+            return rc;
+        return FA2_OK;
+    }
+    DevBuf t[10];  // q k v o dout lse delta dq dk dv
+    const size_t sz[10] = {n, n, n, n, n, nl, nl, n, n, n};
+    for (int i = 0; i < 10; ++i)
+        if ((rc = hip_status(hipMalloc(&t[i].p, sz[i] * 4), "hipMalloc"))) return rc;
+    for (int i = 0; i < 6; ++i)
+        if ((rc = hip_status(hipMemcpy(t[i].p, j.in[i] + (i == 5 ? offl : off), sz[i] * 4, hipMemcpyHostToDevice), "H2D")))
+            return rc;
+    (void)hipEventRecord(e0, st);
+    rc = fa2_backward(t[0].p, t[1].p, t[2].p, t[3].p, t[4].p, t[5].p, t[6].p, t[7].p, t[8].p, t[9].p, 1, j.nheads,
+                      j.S, j.D, j.precision, st);
+    if (rc) return rc;
+    (void)hipEventRecord(e1, st);
+    if ((rc = hip_status(hipEventSynchronize(e1), "kernel"))) return rc;
+    (void)hipEventElapsedTime(&j.ms, e0, e1);
+    for (int i = 0; i < 3; ++i)
+        if ((rc = hip_status(hipMemcpy(j.out[2 + i] + off, t[7 + i].p, n * 4, hipMemcpyDeviceToHost), "D2H"))) return rc;
+    return FA2_OK;
+}
+
+int run_sharded(HostJob proto, int B, int H, int num_devices, float* kernel_ms) {
+    const int total = B * H;
+    int ndev = num_devices < 1 ? 1 : num_devices;
+    const int avail = fa2_device_count();
+    if (avail < ndev) return fail(FA2_E_INVALID, "num_devices exceeds the visible devices");
+    if (ndev > total) ndev = total;
+    std::vector<HostJob> jobs(ndev, proto);
+    for (int g = 0; g < ndev; ++g) {
+        fa2_shard_range(total, ndev, g, &jobs[g].heads0, &jobs[g].nheads);
+        jobs[g].device = g;
+    }
+    auto body = [](HostJob* j) {
+        j->rc = run_shard(*j);
+        if (j->rc) j->err = g_err;
+    };
+    if (ndev == 1) {
+        body(&jobs[0]);
+    } else {
+        std::vector<std::thread> th;
+        for (int g = 0; g < ndev; ++g) th.emplace_back(body, &jobs[g]);
+        for (auto& t : th) t.join();
+    }
+    float mx = 0.f;
+    for (auto& j : jobs) {
+        if (j.rc) return fail(j.rc, "device " + std::to_string(j.device) + ": " + j.err);
+        mx = std::max(mx, j.ms);
+    }
+    if (kernel_ms) *kernel_ms = mx;
+    return FA2_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fa2_forward_host(const float* q, const float* k, const float* v, float* o, float* lse, int B, int H, int S, int D,
+                     int precision, int num_devices, float* kernel_ms) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_precision(precision)) || (rc = check_ptrs({q, k, v, o, lse})))
+        return rc;
+    HostJob j;
+    j.in[0] = q; j.in[1] = k; j.in[2] = v;
+    j.out[0] = o; j.out[1] = lse;
+    j.S = S; j.D = D; j.precision = precision;
+    return run_sharded(j, B, H, num_devices, kernel_ms);
+}
+
+int fa2_backward_host(const float* q, const float* k, const float* v, const float* o, const float* dout,
+                      const float* lse, float* dq, float* dk, float* dv, int B, int H, int S, int D, int precision,
+                      int num_devices, float* kernel_ms) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_precision(precision)) ||
+        (rc = check_ptrs({q, k, v, o, dout, lse, dq, dk, dv})))
+        return rc;
+    HostJob j;
+    j.in[0] = q; j.in[1] = k; j.in[2] = v; j.in[3] = o; j.in[4] = dout; j.in[5] = lse;
+    j.out[2] = dq; j.out[3] = dk; j.out[4] = dv;
+    j.S = S; j.D = D; j.precision = precision; j.backward = true;
+    return run_sharded(j, B, H, num_devices, kernel_ms);
+}
+
+}  // extern "C"

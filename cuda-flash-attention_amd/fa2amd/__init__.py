@@ -1,0 +1,220 @@
+"""fa2amd -- Python host side of the MI355X-native FA2 forward+backward.
+
+Thin ctypes binding of the C ABI in ``include/fa2_amd.h`` (``lib/libfa2amd.so``,
+built by ``make`` in this directory / ``__graft_entry__.build()``).  The product
+path is the HIP extension only: if the library is missing or the tensors are not
+on a GPU, these functions raise -- there is no CPU fallback.
+
+Tensors are torch fp32, contiguous, [B, H, S, D] (logsumexp / delta [B, H, S]),
+exactly the reference's layout (detker/CUDA-Flash-Attention).
+``precision`` is ``"fp16"`` (MFMA f16 tiles, fp32 accumulate -- the reference's
+``_f16.cu`` variants) or ``"fp32"`` (exact fp32 MFMA -- the reference's default).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfa2amd.so")
+CLI_PATH = os.path.join(PKG_ROOT, "bin", "FlashAttention")
+KERNEL_DIR = os.path.join(PKG_ROOT, "kernels")
+
+FA2_FP16 = 0
+FA2_FP32 = 1
+_PRECISION = {"fp16": FA2_FP16, "fp32": FA2_FP32, FA2_FP16: FA2_FP16, FA2_FP32: FA2_FP32}
+SUPPORTED_HEAD_DIMS = (32, 64, 128)
+
+# exported symbols of include/fa2_amd.h (checked by tests/test_capi_symbols.py)
+C_SYMBOLS = (
+    "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv", "fa2_backward_dq",
+    "fa2_forward_host", "fa2_backward_host", "fa2_shard_range", "fa2_last_error",
+    "fa2_version", "fa2_device_count",
+)
+
+
+class FA2Error(RuntimeError):
+    """A non-zero return code of the C ABI (message from fa2_last_error)."""
+
+
+_lib = None
+
+
+def build(jobs: int = 8) -> str:
+    """Compile the HIP extension in-tree (hipcc, gfx950)."""
+    import subprocess
+
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", PKG_ROOT], check=True)
+    return LIB_PATH
+
+
+def lib():
+    """Load lib/libfa2amd.so (raises FA2Error if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FA2Error(f"HIP extension not built: {LIB_PATH} is missing (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, V = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p
+    FP = ctypes.POINTER(ctypes.c_float)
+    sig = {
+        "fa2_forward": [P] * 5 + [I] * 5 + [V],
+        "fa2_delta": [P] * 3 + [I] * 4 + [V],
+        "fa2_backward": [P] * 10 + [I] * 5 + [V],
+        "fa2_backward_dkdv": [P] * 8 + [I] * 4 + [V],
+        "fa2_backward_dq": [P] * 7 + [I] * 4 + [V],
+        "fa2_forward_host": [P] * 5 + [I] * 6 + [FP],
+        "fa2_backward_host": [P] * 9 + [I] * 6 + [FP],
+        "fa2_shard_range": [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)],
+        "fa2_last_error": [],
+        "fa2_version": [],
+        "fa2_device_count": [],
+    }
+    for name, args in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_char_p if name == "fa2_last_error" else I
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise FA2Error(lib().fa2_last_error().decode() or f"fa2 error {rc}")
+
+
+def version() -> int:
+    return lib().fa2_version()
+
+
+def shard_range(total_heads: int, shards: int, index: int):
+    """Contiguous balanced head range of shard ``index`` (same rule as the C ABI)."""
+    q, r = divmod(total_heads, shards)
+    first = index * q + min(index, r)
+    return first, q + (1 if index < r else 0)
+
+
+# ---------------------------------------------------------------------------
+# device-tensor API (torch)
+# ---------------------------------------------------------------------------
+def _dev(t, name):
+    import torch
+
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise FA2Error(f"{name} must be on a GPU (no CPU fallback in the product path)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t.data_ptr()
+
+
+def _stream(stream, device):
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _shape(q):
+    if q.dim() != 4:
+        raise ValueError("expected [B, H, S, D]")
+    B, H, S, D = q.shape
+    if D not in SUPPORTED_HEAD_DIMS:
+        raise ValueError(f"head_dim {D} not in {SUPPORTED_HEAD_DIMS}")
+    return B, H, S, D
+
+
+def forward(q, k, v, precision="fp16", out=None, lse=None, stream=None):
+    """O, LSE = FA2 forward.  Replaces the reference's fwd kernel launch."""
+    import torch
+
+    B, H, S, D = _shape(q)
+    for t, n in ((k, "k"), (v, "v")):
+        if t.shape != q.shape:
+            raise ValueError(f"{n} shape {tuple(t.shape)} != q shape {tuple(q.shape)}")
+    out = torch.empty_like(q) if out is None else out
+    lse = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if lse is None else lse
+    ptrs = [_dev(t, n) for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out"), (lse, "lse"))]
+    _check(lib().fa2_forward(*ptrs, B, H, S, D, _PRECISION[precision], _stream(stream, q.device)))
+    return out, lse
+
+
+def delta(dout, o, out=None, stream=None):
+    import torch
+
+    B, H, S, D = _shape(o)
+    out = torch.empty((B, H, S), device=o.device, dtype=torch.float32) if out is None else out
+    _check(lib().fa2_delta(_dev(dout, "dout"), _dev(o, "o"), _dev(out, "delta"), B, H, S, D, _stream(stream, o.device)))
+    return out
+
+
+def backward(q, k, v, o, dout, lse, precision="fp16", dq=None, dk=None, dv=None, delta_buf=None, stream=None):
+    """dQ, dK, dV = FA2 backward (Δ computed internally into ``delta_buf``)."""
+    import torch
+
+    B, H, S, D = _shape(q)
+    dq = torch.empty_like(q) if dq is None else dq
+    dk = torch.empty_like(q) if dk is None else dk
+    dv = torch.empty_like(q) if dv is None else dv
+    delta_buf = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if delta_buf is None else delta_buf
+    names = ("q", "k", "v", "o", "dout", "lse", "delta", "dq", "dk", "dv")
+    ptrs = [_dev(t, n) for t, n in zip((q, k, v, o, dout, lse, delta_buf, dq, dk, dv), names)]
+    _check(lib().fa2_backward(*ptrs, B, H, S, D, _PRECISION[precision], _stream(stream, q.device)))
+    return dq, dk, dv
+
+
+def backward_dkdv(q, k, v, dout, lse, delta_buf, dk, dv, stream=None):
+    B, H, S, D = _shape(q)
+    ptrs = [_dev(t, n) for t, n in zip((q, k, v, dout, lse, delta_buf, dk, dv),
+                                       ("q", "k", "v", "dout", "lse", "delta", "dk", "dv"))]
+    _check(lib().fa2_backward_dkdv(*ptrs, B, H, S, D, _stream(stream, q.device)))
+
+
+def backward_dq(q, k, v, dout, lse, delta_buf, dq, stream=None):
+    B, H, S, D = _shape(q)
+    ptrs = [_dev(t, n) for t, n in zip((q, k, v, dout, lse, delta_buf, dq),
+                                       ("q", "k", "v", "dout", "lse", "delta", "dq"))]
+    _check(lib().fa2_backward_dq(*ptrs, B, H, S, D, _stream(stream, q.device)))
+
+
+# ---------------------------------------------------------------------------
+# host-array API (numpy): the reference host functions' semantics
+# ---------------------------------------------------------------------------
+def _np(a, name):
+    import numpy as np
+
+    if not (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags.c_contiguous):
+        raise TypeError(f"{name} must be a C-contiguous float32 numpy array")
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def forward_host(q, k, v, precision="fp32", num_devices=1):
+    """(O, LSE, kernel_ms) from host arrays: host_flash_attention2_forward[_fp16] semantics."""
+    import numpy as np
+
+    B, H, S, D = q.shape
+    o = np.empty_like(q)
+    lse = np.empty((B, H, S), np.float32)
+    ms = ctypes.c_float(0.0)
+    _check(lib().fa2_forward_host(_np(q, "q"), _np(k, "k"), _np(v, "v"), _np(o, "o"), _np(lse, "lse"),
+                                  B, H, S, D, _PRECISION[precision], num_devices, ctypes.byref(ms)))
+    return o, lse, ms.value
+
+
+def backward_host(q, k, v, o, dout, lse, precision="fp32", num_devices=1):
+    """(dQ, dK, dV, kernel_ms) from host arrays: host_flash_attention2_backward[_fp16] semantics."""
+    import numpy as np
+
+    B, H, S, D = q.shape
+    dq, dk, dv = np.empty_like(q), np.empty_like(q), np.empty_like(q)
+    ms = ctypes.c_float(0.0)
+    _check(lib().fa2_backward_host(_np(q, "q"), _np(k, "k"), _np(v, "v"), _np(o, "o"), _np(dout, "dout"),
+                                   _np(lse, "lse"), _np(dq, "dq"), _np(dk, "dk"), _np(dv, "dv"),
+                                   B, H, S, D, _PRECISION[precision], num_devices, ctypes.byref(ms)))
+    return dq, dk, dv, ms.value

@@ -1,0 +1,371 @@
+// f-attn2-backward.cu -- FA2 backward, exact-fp32 path, for MI355X (gfx950).
+//
+// Replaces detker/CUDA-Flash-Attention kernels/f-attn2-backward.cu
+// (flash_attention2_backward_kernel :33-339, D_computation_reduction_kernel
+// :341-380, host launcher :384-488, CuPy wrappers :491-528).  Same contract:
+//   Δ_i = Σ_d dO_id·O_id                              (:341-380)
+//   per 32-key block: P = exp(QKᵀ/√D − LSE), dV += PᵀdO, dS = P∘(dOVᵀ − Δ)/√D,
+//   dQ += dS·K through global fp32 atomics (dQ pre-zeroed by the caller, :427-429,
+//   harness :546-548), dK += dSᵀQ; dK/dV written once (:326-338).
+//
+// Launch geometry = the reference harness's (test_flash_attention2.py:499-535):
+// backward grid B·H·⌈S/32⌉ x 256 threads (one workgroup per 32 keys), Δ kernel
+// B·H·S x 64 threads.  The four waves of a workgroup split the query range (wave
+// w takes every 4th 32-row query tile of a 128-row super-tile staged in LDS) and
+// sum their dKᵀ/dVᵀ register accumulators through LDS at the end.  All five
+// products run on v_mfma_f32_32x32x2_f32 (exact fp32): S and dP with the key on
+// the lane so the P / dS accumulator registers feed dVᵀ += dOᵀP and dKᵀ += QᵀdS
+// directly as B operands; dS crosses LDS once, for dQ = dS·K, whose 32x32
+// accumulator is added to HBM with row-segment-shaped global_atomic_add_f32.
+//
+// Self-contained device code (hiprtc -std=c++14 -DCUPY_INLINE_COMPILE).
+#ifndef CUPY_INLINE_COMPILE
+#include "f-attn2.cuh"
+#endif
+
+namespace fa2f32b {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define FA2FB_LOG2E 1.4426950408889634f
+
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+template <int D>
+__device__ __forceinline__ void stage_rows(float* tile, const float* __restrict__ src, int row0, int ROWS, int S,
+                                           int tid, float scale) {
+    for (int x = tid; x < ROWS * (D / 4); x += 256) {
+        const int row = x / (D / 4), c4 = x - row * (D / 4);
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (row0 + row < S) v = *reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * D + 4 * c4);
+        *reinterpret_cast<f32x4*>(tile + row * (D + 4) + 4 * c4) = v * scale;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Δ = rowsum(dO ∘ O).  Reference-geometry body: one row per workgroup, any
+// blockDim <= 1024 (the harness uses 64, test_flash_attention2.py:504-506).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void delta_row_body(const float* __restrict__ dO, const float* __restrict__ O, int rows,
+                                               int D, float* __restrict__ Dvec) {
+    __shared__ float part[16];
+    const long row = blockIdx.x;
+    if (row >= rows) return;
+    float acc = 0.f;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) acc += dO[row * D + d] * O[row * D + d];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    const int nw = (blockDim.x + 63) / 64;
+    if (nw == 1) {
+        if (threadIdx.x == 0) Dvec[row] = acc;
+        return;
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = 0.f;
+        for (int w = 0; w < nw; ++w) s += part[w];
+        Dvec[row] = s;
+    }
+}
+
+// Library Δ kernel: D/4 lanes per row (float4 loads), grid-stride over rows.
+template <int D>
+__global__ void __launch_bounds__(256) fa2_delta_kernel(const float* __restrict__ dO, const float* __restrict__ O,
+                                                        float* __restrict__ Dvec, long rows) {
+    constexpr int LPR = D / 4;  // lanes per row
+    const long stride = (long)gridDim.x * (256 / LPR);
+    const int sub = threadIdx.x % LPR;
+    for (long row = (long)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; row < rows + 0; row += stride) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(dO + row * D + 4 * sub);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(O + row * D + 4 * sub);
+        float acc = a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+#pragma unroll
+        for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+        if (sub == 0) Dvec[row] = acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// backward body: 32 keys per workgroup of 4 waves, grid = BH * ceil(S/32)
+// ---------------------------------------------------------------------------
+template <int D> struct BwdLds {
+    static constexpr int LD = D + 4;
+    static constexpr int T = 128 * LD;        // Q / dO super-tile (also the dK/dV merge buffer)
+    static constexpr int KV = 32 * LD;        // K and V tiles of this workgroup
+    static constexpr int DS = 4 * 32 * 33;    // per-wave dS transpose scratch
+    static constexpr int ROWS = 2 * 128;      // lse2 and delta of the super-tile
+    static constexpr int FLOATS = T + 2 * KV + DS + ROWS;
+};
+
+template <int D>
+__device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const float* __restrict__ K,
+                                             const float* __restrict__ V, const float* __restrict__ dO,
+                                             const float* __restrict__ LSE, const float* __restrict__ Delta,
+                                             float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV,
+                                             int BH, int S, float* smem) {
+    constexpr int LD = D + 4;
+    constexpr int QS = 128;
+    float* T = smem;
+    float* Kt = T + BwdLds<D>::T;
+    float* Vt = Kt + BwdLds<D>::KV;
+    float* Ds = Vt + BwdLds<D>::KV;
+    float* lse2 = Ds + BwdLds<D>::DS;
+    float* del = lse2 + QS;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int nkb = (S + 31) / 32;
+    const int bh = blockIdx.x / nkb, kb = blockIdx.x - bh * nkb;
+    if (bh >= BH) return;
+    const long base = (long)bh * S * D;
+    const long rbase = (long)bh * S;
+    const int k0 = kb * 32;
+    const float qscale = FA2FB_LOG2E / __builtin_sqrtf((float)D);
+    const float dscale = 1.f / __builtin_sqrtf((float)D);
+    float* Dsw = Ds + wave * 32 * 33;
+
+    stage_rows<D>(Kt, K + base, k0, 32, S, tid, 1.f);
+    stage_rows<D>(Vt, V + base, k0, 32, S, tid, 1.f);
+
+    f32x16 dka[D / 32], dva[D / 32];
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            dka[b][i] = 0.f;
+            dva[b][i] = 0.f;
+        }
+
+    const int nsuper = (S + QS - 1) / QS;
+    for (int st = 0; st < nsuper; ++st) {
+        const int q0 = st * QS;
+        const int qw = q0 + 32 * wave;  // this wave's 32 query rows
+        const bool active = qw < S;
+        const float* Tw = T + 32 * wave * LD;
+        // ---- Q (scaled) + row constants
+        __syncthreads();
+        stage_rows<D>(T, Q + base, q0, QS, S, tid, qscale);
+        if (tid < QS) {
+            const int qi = q0 + tid;
+            lse2[tid] = qi < S ? LSE[rbase + qi] * FA2FB_LOG2E : __builtin_inff();
+            del[tid] = qi < S ? Delta[rbase + qi] : 0.f;
+        }
+        __syncthreads();
+        f32x16 p;  // P[q][key]: rows q (registers), col key (lane)
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) p[i] = -lse2[32 * wave + acc_row(i, h)];
+#pragma unroll
+            for (int m = 0; m < D / 8; ++m) {
+                const f32x4 a = *reinterpret_cast<const f32x4*>(Tw + r * LD + 8 * m + 4 * h);
+                const f32x4 b = *reinterpret_cast<const f32x4*>(Kt + r * LD + 8 * m + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) p = mfma(a[e], b[e], p);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) p[i] = (k0 + r < S) ? fast_exp2(p[i]) : 0.f;
+        }
+        // ---- dO
+        __syncthreads();
+        stage_rows<D>(T, dO + base, q0, QS, S, tid, 1.f);
+        __syncthreads();
+        f32x16 ds;
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) ds[i] = -del[32 * wave + acc_row(i, h)];
+#pragma unroll
+            for (int m = 0; m < D / 8; ++m) {
+                const f32x4 a = *reinterpret_cast<const f32x4*>(Tw + r * LD + 8 * m + 4 * h);
+                const f32x4 b = *reinterpret_cast<const f32x4*>(Vt + r * LD + 8 * m + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) ds = mfma(a[e], b[e], ds);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) ds[i] *= p[i];
+            // dV^T += dO^T P
+#pragma unroll
+            for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dva[b] = mfma(Tw[acc_row(i, h) * LD + 32 * b + r], p[i], dva[b]);
+            // dS -> per-wave scratch [q][key] for dQ
+#pragma unroll
+            for (int i = 0; i < 16; ++i) Dsw[acc_row(i, h) * 33 + r] = ds[i];
+        }
+        // ---- Q (unscaled) for dK
+        __syncthreads();
+        stage_rows<D>(T, Q + base, q0, QS, S, tid, 1.f);
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dka[b] = mfma(Tw[acc_row(i, h) * LD + 32 * b + r], ds[i], dka[b]);
+            // dQ[q][d] += dS[q][:] K[:][d] / sqrt(D), one 32x32 block per 32 columns
+#pragma unroll
+            for (int b = 0; b < D / 32; ++b) {
+                f32x16 acc;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+                for (int s = 0; s < 16; ++s)
+                    acc = mfma(Dsw[r * 33 + 2 * s + h], Kt[(2 * s + h) * LD + 32 * b + r], acc);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int qi = qw + acc_row(i, h);
+                    if (qi < S) atomicAdd(dQ + base + (long)qi * D + 32 * b + r, acc[i] * dscale);
+                }
+            }
+        }
+    }
+
+    // ---- sum the four waves' dK^T / dV^T through LDS and write rows [k0, k0+32)
+    for (int pass = 0; pass < 2; ++pass) {
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x16& a = pass == 0 ? dka[b] : dva[b];
+                const f32x4 v = {a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]};
+                *reinterpret_cast<f32x4*>(T + (wave * 32 + r) * LD + 32 * b + 8 * g + 4 * h) = v;
+            }
+        __syncthreads();
+        float* dst = pass == 0 ? dK : dV;
+        const float sc = pass == 0 ? dscale : 1.f;
+        for (int x = tid; x < 32 * (D / 4); x += 256) {
+            const int row = x / (D / 4), c4 = x - row * (D / 4);
+            if (k0 + row < S) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int w = 0; w < 4; ++w) acc += *reinterpret_cast<const f32x4*>(T + (w * 32 + row) * LD + 4 * c4);
+                *reinterpret_cast<f32x4*>(dst + base + (long)(k0 + row) * D + 4 * c4) = acc * sc;
+            }
+        }
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256)
+fa2_bwd_f32_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                   const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+                   float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV, int BH, int S) {
+    __shared__ __attribute__((aligned(16))) float smem[BwdLds<D>::FLOATS];
+    bwd_f32_body<D>(Q, K, V, dO, LSE, Delta, dQ, dK, dV, BH, S, smem);
+}
+
+}  // namespace fa2f32b
+
+#ifndef CUPY_INLINE_COMPILE
+namespace fa2 {
+
+namespace {
+template <int D>
+hipError_t delta_dispatch(const float* dout, const float* o, float* delta, int bh, int S, hipStream_t stream) {
+    const long rows = (long)bh * S;
+    const long rows_per_block = 256 / (D / 4);
+    long grid = (rows + rows_per_block - 1) / rows_per_block;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL((fa2f32b::fa2_delta_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, dout, o, delta,
+                       rows);
+    return hipGetLastError();
+}
+template <int D>
+hipError_t bwd_f32_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                            const float* delta, float* dq, float* dk, float* dv, int bh, int S, hipStream_t stream) {
+    const long grid = (long)bh * ((S + 31) / 32);
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f32b::fa2_bwd_f32_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, dout,
+                       lse, delta, dq, dk, dv, bh, S);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_delta(int D, const float* dout, const float* o, float* delta, int bh, int S, hipStream_t stream) {
+    if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
+    switch (D) {
+        case 32: return delta_dispatch<32>(dout, o, delta, bh, S, stream);
+        case 64: return delta_dispatch<64>(dout, o, delta, bh, S, stream);
+        case 128: return delta_dispatch<128>(dout, o, delta, bh, S, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_backward_f32(int D, const float* q, const float* k, const float* v, const float* o,
+                               const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
+                               int bh, int S, hipStream_t stream) {
+    if (bh <= 0 || S <= 0 || !supported_head_dim(D)) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(dq, 0, (size_t)bh * S * D * sizeof(float), stream);
+    if (e != hipSuccess) return e;
+    e = launch_delta(D, dout, o, delta, bh, S, stream);
+    if (e != hipSuccess) return e;
+    switch (D) {
+        case 32: return bwd_f32_dispatch<32>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        case 64: return bwd_f32_dispatch<64>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        default: return bwd_f32_dispatch<128>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+    }
+}
+
+}  // namespace fa2
+
+// Host API with the reference's semantics (f-attn2-backward.cu:384-485).
+template <int head_dim>
+void host_flash_attention2_backward(const float* h_Q, const float* h_K, const float* h_V, const float* h_O,
+                                    const float* h_dO, const float* h_lse, float* h_dQ, float* h_dK, float* h_dV,
+                                    int batch_size, int seq_len, int num_heads, TimerManager* tm) {
+    const size_t n = (size_t)batch_size * num_heads * seq_len * head_dim;
+    const size_t nl = (size_t)batch_size * num_heads * seq_len;
+    float* d[10];
+    const size_t sz[10] = {n, n, n, n, n, nl, nl, n, n, n};
+    for (int i = 0; i < 10; ++i) HIP_CHECK(hipMalloc(&d[i], sz[i] * sizeof(float)));
+    const float* src[6] = {h_Q, h_K, h_V, h_O, h_dO, h_lse};
+    for (int i = 0; i < 6; ++i) HIP_CHECK(hipMemcpy(d[i], src[i], sz[i] * sizeof(float), hipMemcpyHostToDevice));
+    tm->Start();
+    HIP_CHECK(fa2::launch_backward_f32(head_dim, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9],
+                                       batch_size * num_heads, seq_len, nullptr));
+    tm->Stop();
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy(h_dQ, d[7], n * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(h_dK, d[8], n * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(h_dV, d[9], n * sizeof(float), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 10; ++i) HIP_CHECK(hipFree(d[i]));
+}
+#define FA2_INST_BWD32(D)                                                                                    \
+    template void host_flash_attention2_backward<D>(const float*, const float*, const float*, const float*, \
+                                                    const float*, const float*, float*, float*, float*, int, \
+                                                    int, int, TimerManager*);
+FA2_INST_BWD32(32)
+FA2_INST_BWD32(64)
+FA2_INST_BWD32(128)
+#else
+// CuPy face (test_flash_attention2.py:132-141, 499-535).  dQ/dK/dV arrive zeroed.
+extern "C" __global__ void __launch_bounds__(256)
+flash_attention2_backward_kernel_wrapper(const float* query, const float* key, const float* value,
+                                         const float* output, const float* d_output, const float* logsumexp,
+                                         const float* d, float* d_query, float* d_key, float* d_value,
+                                         int batch_size, int num_heads, int seq_len, int head_dim) {
+    __shared__ __attribute__((aligned(16))) float smem[fa2f32b::BwdLds<128>::FLOATS];
+    (void)output;
+    const int bh = batch_size * num_heads;
+    if (head_dim == 64)
+        fa2f32b::bwd_f32_body<64>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
+                                  smem);
+    else if (head_dim == 32)
+        fa2f32b::bwd_f32_body<32>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
+                                  smem);
+    else if (head_dim == 128)
+        fa2f32b::bwd_f32_body<128>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
+                                   smem);
+}
+
+// Note the output pointer comes last, as in the reference (f-attn2-backward.cu:515-528).
+extern "C" __global__ void D_computation_reduction_kernel_wrapper(const float* d_output, const float* output,
+                                                                  int batch_size, int num_heads, int seq_len,
+                                                                  int head_dim, float* d) {
+    fa2f32b::delta_row_body(d_output, output, batch_size * num_heads * seq_len, head_dim, d);
+}
+#endif  // CUPY_INLINE_COMPILE

@@ -1,0 +1,476 @@
+// f-attn2-backward_f16.cu -- FA2 backward, fp16-tile MFMA path, for MI355X (gfx950).
+//
+// Replaces detker/CUDA-Flash-Attention kernels/f-attn2-backward_f16.cu
+// (flash_attention2_backward_kernel_fp16 :34-330, D kernel :332-371, host
+// launcher :375-474, CuPy wrappers :477-514).  Same math as the reference
+// backward (f-attn2-backward.cu:119-338):
+//   P  = exp(Q Kᵀ/√D − LSE)           (recomputed, :151-184)
+//   dV = Pᵀ dO                        (:218-240)
+//   dS = P ∘ (dO Vᵀ − Δ),  Δ = rowsum(dO∘O)   (:242-267, :341-380)
+//   dQ = dS K / √D                    (:269-301, atomics there)
+//   dK = dSᵀ Q / √D                   (:303-323)
+//
+// MI355X design: two MFMA kernels instead of one kernel
+// with ~B·H·S²·D/32 global fp32 atomics (the chip-wide fp32 atomic rate,
+// ≈1.3 TB/s, would bound the whole backward):
+//   * fa2_bwd_dkdv_f16: one wave = 32 keys whose K, V fragments stay in VGPRs
+//     and whose dKᵀ, dVᵀ accumulate in registers; the workgroup streams 64-row
+//     Q/dO blocks through LDS.  S and dP are computed with the key on the lane,
+//     their accumulators start at −LSE·log2e and −Δ (row constants as initial
+//     accumulator), and the packed P / dS accumulators are directly the B
+//     operands of dVᵀ += dOᵀP and dKᵀ += QᵀdS (dOᵀ, Qᵀ via ds_read_b64_tr_b16).
+//   * fa2_bwd_dq_f16: one wave = 32 queries (Q, dO fragments in VGPRs) streaming
+//     64-key K/V tiles; Sᵀ and dPᵀ with the query on the lane, dQᵀ += Kᵀ dSᵀ.
+//   Deterministic (no atomics), dq/dk/dv fully written (no memsets).
+//
+// Self-contained device code (hiprtc-compilable with -DCUPY_INLINE_COMPILE, C++14).
+#ifndef CUPY_INLINE_COMPILE
+#include "f-attn2.cuh"
+#endif
+
+namespace fa2f16b {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+#define FA2B_LOG2E 1.4426950408889634f
+
+__device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+template <int D> struct Swz;
+template <> struct Swz<32> {
+    static __device__ __forceinline__ int f(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) << 1); }
+};
+template <> struct Swz<64> {
+    static __device__ __forceinline__ int f(int r) {
+        return ((r >> 1) & 1) | (((r >> 2) & 1) << 1) | ((((r >> 1) ^ (r >> 3)) & 1) << 2);
+    }
+};
+template <> struct Swz<128> {
+    static __device__ __forceinline__ int f(int r) {
+        return (r & 1) | (((r >> 1) & 1) << 1) | (((r ^ (r >> 2)) & 1) << 2) | ((((r >> 1) ^ (r >> 3)) & 1) << 3);
+    }
+};
+template <int D>
+__device__ __forceinline__ int tile_off(int row, int col) {
+    return row * D + (((col >> 3) ^ Swz<D>::f(row)) << 3) + (col & 7);
+}
+__device__ __forceinline__ f16x8 lds_row8(const _Float16* p) { return *reinterpret_cast<const f16x8*>(p); }
+__device__ __forceinline__ i16x4 lds_tr4(const _Float16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p));
+}
+__device__ __forceinline__ f16x8 cat4(i16x4 a, i16x4 b) {
+    i16x8 c = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(f16x8, c);
+}
+template <int D>
+__device__ __forceinline__ f16x8 tr_operand(const _Float16* tile, int r0, int c0, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    const int row = r0 + 4 * (g >> 1) + (i >> 2);
+    const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+    return cat4(lds_tr4(tile + tile_off<D>(row, col)), lds_tr4(tile + tile_off<D>(row + 8, col)));
+}
+__device__ __forceinline__ f16x8 to_f16x8(f32x4 a, f32x4 b, float s) {
+    f16x8 r;
+    r[0] = (_Float16)(a[0] * s); r[1] = (_Float16)(a[1] * s); r[2] = (_Float16)(a[2] * s); r[3] = (_Float16)(a[3] * s);
+    r[4] = (_Float16)(b[0] * s); r[5] = (_Float16)(b[1] * s); r[6] = (_Float16)(b[2] * s); r[7] = (_Float16)(b[3] * s);
+    return r;
+}
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int q = nwg >> 3, rr = nwg & 7, xcd = orig & 7, idx = orig >> 3;
+    return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+}
+// fragment of 8 consecutive fp32 (row `row` of a [S][D] tensor, cols c..c+7) as fp16
+__device__ __forceinline__ f16x8 load_frag(const float* __restrict__ p, bool valid, float s) {
+    if (!valid) return f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    const f32x4* v = reinterpret_cast<const f32x4*>(p);
+    return to_f16x8(v[0], v[1], s);
+}
+
+template <int D, int ROWS, int NT>
+struct TileStager {
+    static constexpr int CPR = D / 8;
+    static constexpr int CHUNKS = ROWS * CPR;
+    static constexpr int CPT = (CHUNKS + NT - 1) / NT;
+    f32x4 r[CPT][2];
+    __device__ __forceinline__ void load(const float* __restrict__ src, int row0, int S, int tid) {
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int x = tid + c * NT;
+            const int row = x / CPR, ch = x % CPR;
+            if ((CHUNKS % NT == 0 || x < CHUNKS) && row0 + row < S) {
+                const f32x4* p = reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * D + ch * 8);
+                r[c][0] = p[0];
+                r[c][1] = p[1];
+            } else {
+                r[c][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                r[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    }
+    __device__ __forceinline__ void store(_Float16* tile, int tid) const {
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int x = tid + c * NT;
+            if (CHUNKS % NT == 0 || x < CHUNKS) {
+                const int row = x / CPR, ch = x % CPR;
+                *reinterpret_cast<f16x8*>(tile + row * D + ((ch ^ Swz<D>::f(row)) << 3)) =
+                    to_f16x8(r[c][0], r[c][1], 1.f);
+            }
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// dK, dV:  grid BH * ceil(S / (32*NW)), block 64*NW
+// ---------------------------------------------------------------------------
+template <int D, int NW>
+__global__ void __launch_bounds__(64 * NW)
+fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                        const float* __restrict__ dO, const float* __restrict__ LSE,
+                        const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV, int S) {
+    constexpr int QT = 64;  // query rows per step
+    constexpr int NT = 64 * NW;
+    constexpr int TILE = QT * D;
+    // [buf][Q | dO] fp16 tiles, then [buf][lse2 | delta] fp32 rows
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
+    __shared__ __attribute__((aligned(16))) float rows[2][2][QT];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int nkb = (S + 32 * NW - 1) / (32 * NW);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = bid / nkb, kb = bid - bh * nkb;
+    const long base = (long)bh * S * D;
+    const long rbase = (long)bh * S;
+    const int key = kb * 32 * NW + wave * 32 + r;
+    const bool kvalid = key < S;
+    const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
+
+    // K (pre-scaled by log2e/sqrt(D)) and V fragments: B operands, lane holds row `key`
+    f16x8 kf[D / 16], vf[D / 16];
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+        kf[t] = load_frag(K + base + (long)key * D + 16 * t + 8 * h, kvalid, kscale);
+        vf[t] = load_frag(V + base + (long)key * D + 16 * t + 8 * h, kvalid, 1.f);
+    }
+    f32x16 dka[D / 32], dva[D / 32];
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            dka[b][i] = 0.f;
+            dva[b][i] = 0.f;
+        }
+
+    TileStager<D, QT, NT> qs, dos;
+    float rowv = 0.f;  // lse2 (threads [0,QT)) or delta (threads [QT,2QT)) of the staged step
+    auto load_rows = [&](int q0) {
+        if (tid < 2 * QT) {
+            const int qi = q0 + (tid & (QT - 1));
+            if (tid < QT) rowv = qi < S ? LSE[rbase + qi] * FA2B_LOG2E : __builtin_inff();
+            else rowv = qi < S ? Delta[rbase + qi] : 0.f;
+        }
+    };
+    auto store_rows = [&](int buf) {
+        if (tid < 2 * QT) rows[buf][tid / QT][tid & (QT - 1)] = rowv;
+    };
+
+    const int nsteps = (S + QT - 1) / QT;
+    qs.load(Q + base, 0, S, tid);
+    dos.load(dO + base, 0, S, tid);
+    load_rows(0);
+    qs.store(smem, tid);
+    dos.store(smem + TILE, tid);
+    store_rows(0);
+    __syncthreads();
+
+    for (int it = 0; it < nsteps; ++it) {
+        const int cur = it & 1;
+        const _Float16* Qs = smem + cur * 2 * TILE;
+        const _Float16* dOs = Qs + TILE;
+        const float* lse2 = rows[cur][0];
+        const float* del = rows[cur][1];
+        const bool more = it + 1 < nsteps;
+        if (more) {
+            qs.load(Q + base, (it + 1) * QT, S, tid);
+            dos.load(dO + base, (it + 1) * QT, S, tid);
+            load_rows((it + 1) * QT);
+        }
+
+        f16x8 pf[2][2], dsf[2][2];
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            // accumulator rows: query qb*32 + (i&3) + 8*(i>>2) + 4h ; col: key (lane)
+            f32x16 sa, da;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2 + qb * 32 + 8 * g + 4 * h);
+                const f32x4 dv = *reinterpret_cast<const f32x4*>(del + qb * 32 + 8 * g + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    sa[4 * g + e] = -lv[e];
+                    da[4 * g + e] = -dv[e];
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < D / 16; ++t) {
+                const int off = tile_off<D>(qb * 32 + r, 16 * t + 8 * h);
+                sa = mfma(lds_row8(Qs + off), kf[t], sa);
+                da = mfma(lds_row8(dOs + off), vf[t], da);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float p = fast_exp2(sa[i]);
+                pf[qb][i >> 3][i & 7] = (_Float16)p;
+                dsf[qb][i >> 3][i & 7] = (_Float16)(p * da[i]);
+            }
+        }
+        // dV^T += dO^T P ;  dK^T += Q^T dS   (k = query rows of this step)
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    dva[b] = mfma(tr_operand<D>(dOs, qb * 32 + 16 * s, 32 * b, lane), pf[qb][s], dva[b]);
+                    dka[b] = mfma(tr_operand<D>(Qs, qb * 32 + 16 * s, 32 * b, lane), dsf[qb][s], dka[b]);
+                }
+
+        if (more) {
+            _Float16* nxt = smem + (cur ^ 1) * 2 * TILE;
+            qs.store(nxt, tid);
+            dos.store(nxt + TILE, tid);
+            store_rows(cur ^ 1);
+        }
+        __syncthreads();
+    }
+
+    if (kvalid) {
+        const float dscale = 1.f / __builtin_sqrtf((float)D);
+        float* dkrow = dK + base + (long)key * D;
+        float* dvrow = dV + base + (long)key * D;
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 a = {dka[b][4 * g] * dscale, dka[b][4 * g + 1] * dscale, dka[b][4 * g + 2] * dscale,
+                           dka[b][4 * g + 3] * dscale};
+                f32x4 c = {dva[b][4 * g], dva[b][4 * g + 1], dva[b][4 * g + 2], dva[b][4 * g + 3]};
+                *reinterpret_cast<f32x4*>(dkrow + 32 * b + 8 * g + 4 * h) = a;
+                *reinterpret_cast<f32x4*>(dvrow + 32 * b + 8 * g + 4 * h) = c;
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// dQ:  grid BH * ceil(S / (32*NW)), block 64*NW
+// ---------------------------------------------------------------------------
+template <int D, int NW>
+__global__ void __launch_bounds__(64 * NW)
+fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                      const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+                      float* __restrict__ dQ, int S) {
+    constexpr int KT = 64;
+    constexpr int NT = 64 * NW;
+    constexpr int TILE = KT * D;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int nqb = (S + 32 * NW - 1) / (32 * NW);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = bid / nqb, qb = bid - bh * nqb;
+    const long base = (long)bh * S * D;
+    const int q = qb * 32 * NW + wave * 32 + r;
+    const bool qvalid = q < S;
+    const float qscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
+
+    f16x8 qf[D / 16], df[D / 16];
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+        qf[t] = load_frag(Q + base + (long)q * D + 16 * t + 8 * h, qvalid, qscale);
+        df[t] = load_frag(dO + base + (long)q * D + 16 * t + 8 * h, qvalid, 1.f);
+    }
+    const float lse2 = qvalid ? LSE[(long)bh * S + q] * FA2B_LOG2E : __builtin_inff();
+    const float del = qvalid ? Delta[(long)bh * S + q] : 0.f;
+
+    f32x16 dqa[D / 32];
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dqa[b][i] = 0.f;
+
+    const int ntiles = (S + KT - 1) / KT;
+    TileStager<D, KT, NT> ks, vs;
+    ks.load(K + base, 0, S, tid);
+    vs.load(V + base, 0, S, tid);
+    ks.store(smem, tid);
+    vs.store(smem + TILE, tid);
+    __syncthreads();
+
+    for (int j = 0; j < ntiles; ++j) {
+        const _Float16* Ks = smem + (j & 1) * 2 * TILE;
+        const _Float16* Vs = Ks + TILE;
+        const bool more = j + 1 < ntiles;
+        if (more) {
+            ks.load(K + base, (j + 1) * KT, S, tid);
+            vs.load(V + base, (j + 1) * KT, S, tid);
+        }
+        const int k0 = j * KT;
+        f16x8 dsf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            // rows: key k0 + kb*32 + (i&3) + 8*(i>>2) + 4h ; col: query (lane)
+            f32x16 sa, da;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                sa[i] = -lse2;
+                da[i] = -del;
+            }
+#pragma unroll
+            for (int t = 0; t < D / 16; ++t) {
+                const int off = tile_off<D>(kb * 32 + r, 16 * t + 8 * h);
+                sa = mfma(lds_row8(Ks + off), qf[t], sa);
+                da = mfma(lds_row8(Vs + off), df[t], da);
+            }
+            const bool edge = k0 + KT > S;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float p = fast_exp2(sa[i]);
+                if (edge && k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) p = 0.f;
+                dsf[kb][i >> 3][i & 7] = (_Float16)(p * da[i]);
+            }
+        }
+        // dQ^T += K^T dS^T  (k = key rows of this tile)
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    dqa[b] = mfma(tr_operand<D>(Ks, kb * 32 + 16 * s, 32 * b, lane), dsf[kb][s], dqa[b]);
+        if (more) {
+            _Float16* nxt = smem + ((j + 1) & 1) * 2 * TILE;
+            ks.store(nxt, tid);
+            vs.store(nxt + TILE, tid);
+        }
+        __syncthreads();
+    }
+
+    if (qvalid) {
+        const float dscale = 1.f / __builtin_sqrtf((float)D);
+        float* row = dQ + base + (long)q * D;
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 a = {dqa[b][4 * g] * dscale, dqa[b][4 * g + 1] * dscale, dqa[b][4 * g + 2] * dscale,
+                           dqa[b][4 * g + 3] * dscale};
+                *reinterpret_cast<f32x4*>(row + 32 * b + 8 * g + 4 * h) = a;
+            }
+    }
+}
+
+}  // namespace fa2f16b
+
+#ifndef CUPY_INLINE_COMPILE
+namespace fa2 {
+
+namespace {
+// waves per workgroup: 8 x 32 keys for D <= 64 (2 waves/SIMD fit in 256 VGPRs);
+// D = 128 needs more than 256 registers per lane, so 4 waves (1 per SIMD).
+template <int D> struct DkdvWaves { static constexpr int value = D <= 64 ? 8 : 4; };
+constexpr int kDqWaves = 4;
+
+template <int D>
+hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                         const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
+    constexpr int NW = DkdvWaves<D>::value;
+    const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream,
+                       q, k, v, dout, lse, delta, dk, dv, S);
+    return hipGetLastError();
+}
+template <int D>
+hipError_t dq_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                       const float* delta, float* dq, int bh, int S, hipStream_t stream) {
+    const long grid = (long)bh * ((S + 32 * kDqWaves - 1) / (32 * kDqWaves));
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, kDqWaves>), dim3((unsigned)grid), dim3(64 * kDqWaves), 0,
+                       stream, q, k, v, dout, lse, delta, dq, S);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_bwd_dkdv_f16(int D, const float* q, const float* k, const float* v, const float* dout,
+                               const float* lse, const float* delta, float* dk, float* dv, int bh, int S,
+                               hipStream_t stream) {
+    if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
+    switch (D) {
+        case 32: return dkdv_dispatch<32>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        case 64: return dkdv_dispatch<64>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        case 128: return dkdv_dispatch<128>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_bwd_dq_f16(int D, const float* q, const float* k, const float* v, const float* dout,
+                             const float* lse, const float* delta, float* dq, int bh, int S, hipStream_t stream) {
+    if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
+    switch (D) {
+        case 32: return dq_dispatch<32>(q, k, v, dout, lse, delta, dq, bh, S, stream);
+        case 64: return dq_dispatch<64>(q, k, v, dout, lse, delta, dq, bh, S, stream);
+        case 128: return dq_dispatch<128>(q, k, v, dout, lse, delta, dq, bh, S, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_backward_f16(int D, const float* q, const float* k, const float* v, const float* o,
+                               const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
+                               int bh, int S, hipStream_t stream) {
+    hipError_t e = launch_delta(D, dout, o, delta, bh, S, stream);
+    if (e != hipSuccess) return e;
+    e = launch_bwd_dkdv_f16(D, q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+    if (e != hipSuccess) return e;
+    return launch_bwd_dq_f16(D, q, k, v, dout, lse, delta, dq, bh, S, stream);
+}
+
+}  // namespace fa2
+
+// Host API with the reference's semantics (f-attn2-backward_f16.cu:375-474).
+template <int head_dim>
+void host_flash_attention2_backward_fp16(const float* h_Q, const float* h_K, const float* h_V, const float* h_O,
+                                         const float* h_dO, const float* h_lse, float* h_dQ, float* h_dK, float* h_dV,
+                                         int batch_size, int seq_len, int num_heads, TimerManager* tm) {
+    const size_t n = (size_t)batch_size * num_heads * seq_len * head_dim;
+    const size_t nl = (size_t)batch_size * num_heads * seq_len;
+    float* d[10];
+    const size_t sz[10] = {n, n, n, n, n, nl, nl, n, n, n};
+    for (int i = 0; i < 10; ++i) HIP_CHECK(hipMalloc(&d[i], sz[i] * sizeof(float)));
+    const float* src[6] = {h_Q, h_K, h_V, h_O, h_dO, h_lse};
+    for (int i = 0; i < 6; ++i) HIP_CHECK(hipMemcpy(d[i], src[i], sz[i] * sizeof(float), hipMemcpyHostToDevice));
+    tm->Start();
+    HIP_CHECK(fa2::launch_backward_f16(head_dim, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9],
+                                       batch_size * num_heads, seq_len, nullptr));
+    tm->Stop();
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy(h_dQ, d[7], n * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(h_dK, d[8], n * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(h_dV, d[9], n * sizeof(float), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 10; ++i) HIP_CHECK(hipFree(d[i]));
+}
+#define FA2_INST_BWD16(D)                                                                                         \
+    template void host_flash_attention2_backward_fp16<D>(const float*, const float*, const float*, const float*, \
+                                                         const float*, const float*, float*, float*, float*, int, \
+                                                         int, int, TimerManager*);
+FA2_INST_BWD16(32)
+FA2_INST_BWD16(64)
+FA2_INST_BWD16(128)
+#endif  // CUPY_INLINE_COMPILE

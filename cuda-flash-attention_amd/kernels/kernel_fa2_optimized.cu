@@ -1,0 +1,293 @@
+// kernel_fa2_optimized.cu -- FA2 forward, exact-fp32 path, for MI355X (gfx950).
+//
+// Replaces detker/CUDA-Flash-Attention kernels/kernel_fa2_optimized.cu
+// (flash_attention2_forward_kernel :19-347, host launcher :350-426, CuPy wrapper
+// flash_attention2_forward_kernel_wrapper :428-444).  Same math and outputs:
+// O = softmax(Q Kᵀ/√D) V and LSE = ln l + m per row (:336-343), fp32 in HBM.
+//
+// The launch geometry is the reference harness's, which the CuPy face fixes
+// (test_flash_attention2.py:266-289): grid B·H·⌈S/32⌉, 256 threads, 29 056 B of
+// dynamic LDS at D=64.  Each workgroup owns 32 query rows; its four waves split
+// the key range (wave w takes every 4th 32-key sub-tile of a 128-key super-tile
+// staged cooperatively in LDS) and their (m, l, O) partials are merged through
+// LDS at the end.  Both contractions run on v_mfma_f32_32x32x2_f32 -- exact fp32
+// products, fp32 accumulation, 157 TF/s peak (the reference runs scalar FMAs with
+// 3/4 of its threads idle).  The math is in the log2 domain: Q is
+// pre-scaled by log2(e)/√D so every probability is one v_exp_f32.
+//
+// Self-contained device code: compiles from source text under hiprtc with
+// -std=c++14 -DCUPY_INLINE_COMPILE (test_flash_attention2.py:113-126).  The
+// dynamic-LDS argument of the CuPy launch is accepted and unused: all LDS is
+// static (`static __shared__`), which hiprtc sizes at compile time.
+#ifndef CUPY_INLINE_COMPILE
+#include "f-attn2.cuh"
+#endif
+
+namespace fa2f32 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define FA2F_LOG2E 1.4426950408889634f
+#define FA2F_LN2 0.6931471805599453f
+
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// row index (0..31) held by accumulator register i of lane-half h (32x32 MFMA C/D map)
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// Cooperative staging of rows [row0, row0+ROWS) of a [S][D] fp32 tensor into an
+// LDS tile with row stride D+4 (zero rows past S); 256 threads, float4 granules.
+template <int D>
+__device__ __forceinline__ void stage_rows(float* tile, const float* __restrict__ src, int row0, int ROWS, int S,
+                                           int tid) {
+    for (int x = tid; x < ROWS * (D / 4); x += 256) {
+        const int row = x / (D / 4), c4 = x - row * (D / 4);
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (row0 + row < S) v = *reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * D + 4 * c4);
+        *reinterpret_cast<f32x4*>(tile + row * (D + 4) + 4 * c4) = v;
+    }
+}
+
+// LDS floats needed by the forward body: one [128][D+4] super-tile (K, then V)
+// or, for the final merge, 4 waves x 32 rows x (D+4) plus (m, l) pairs.
+template <int D> struct FwdLds {
+    static constexpr int LD = D + 4;
+    static constexpr int TILE = 128 * LD;
+    static constexpr int MERGE = 4 * 32 * LD + 4 * 32 * 2;
+    static constexpr int FLOATS = TILE > MERGE ? TILE : MERGE;
+};
+
+// Forward body: 32 query rows per workgroup of 4 waves; grid = BH * ceil(S/32).
+// The super-tile [128 keys][D+4] fp32 (row pad 4 floats: conflict-free
+// ds_read_b128 row fragments and ds_read_b32 column walks) holds K for the
+// score phase, then V for the PV phase, as the reference reuses kv_buff
+// (kernel_fa2_optimized.cu:95-123, :261-283).
+template <int D>
+__device__ __forceinline__ void fwd_f32_body(const float* __restrict__ Q, const float* __restrict__ K,
+                                             const float* __restrict__ V, float* __restrict__ O,
+                                             float* __restrict__ LSE, int BH, int S, float* smem) {
+    constexpr int KS = 128;  // keys per super-tile (4 waves x 32)
+    constexpr int LD = D + 4;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int nqb = (S + 31) / 32;
+    const int bh = blockIdx.x / nqb, qb = blockIdx.x - bh * nqb;
+    if (bh >= BH) return;
+    const long base = (long)bh * S * D;
+    const int q = qb * 32 + r;
+    const float qscale = FA2F_LOG2E / __builtin_sqrtf((float)D);
+
+    // Q fragment (B operand): lane holds Q[q][8m + 4h + e], m < D/8, e < 4
+    float qf[D / 2];
+#pragma unroll
+    for (int m = 0; m < D / 8; ++m) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (q < S) v = *reinterpret_cast<const f32x4*>(Q + base + (long)q * D + 8 * m + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qf[4 * m + e] = v[e] * qscale;
+    }
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[b][i] = 0.f;
+    float m_run = -__builtin_inff(), l_run = 0.f;
+
+    const int nsuper = (S + KS - 1) / KS;
+    for (int st = 0; st < nsuper; ++st) {
+        const int k0 = st * KS;
+        const int kw = k0 + 32 * wave;  // this wave's 32-key sub-tile
+        const float* Tw = smem + 32 * wave * LD;
+        // ---- K phase
+        __syncthreads();
+        stage_rows<D>(smem, K + base, k0, KS, S, tid);
+        __syncthreads();
+        f32x16 sacc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
+        if (kw < S) {
+#pragma unroll
+            for (int m = 0; m < D / 8; ++m) {
+                const f32x4 kv = *reinterpret_cast<const f32x4*>(Tw + r * LD + 8 * m + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], qf[4 * m + e], sacc);
+            }
+            if (kw + 32 > S) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (kw + acc_row(i, h) >= S) sacc[i] = -__builtin_inff();
+            }
+            float mx = sacc[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i) mx = fmaxf(mx, sacc[i]);
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float mnew = fmaxf(m_run, mx);
+            if (__any(mnew > m_run)) {
+                const float alpha = fast_exp2(m_run - mnew);
+                l_run *= alpha;
+#pragma unroll
+                for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) oacc[b][i] *= alpha;
+            }
+            m_run = mnew;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                sacc[i] = fast_exp2(sacc[i] - m_run);
+                l_run += sacc[i];
+            }
+        }
+        // ---- V phase
+        __syncthreads();
+        stage_rows<D>(smem, V + base, k0, KS, S, tid);
+        __syncthreads();
+        if (kw < S) {
+            // O^T += V^T P^T : step i uses accumulator register i as B (k = h <-> key acc_row(i,h))
+#pragma unroll
+            for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) oacc[b] = mfma(Tw[acc_row(i, h) * LD + 32 * b + r], sacc[i], oacc[b]);
+        }
+    }
+
+    // merge the four waves' partials: (m, l, O) through LDS (reuses the staging buffer)
+    __syncthreads();
+    float* Om = smem;                      // [4][32][D+4]
+    float* ml = smem + 4 * 32 * LD;        // [4][32][2]
+    const float l_tot = l_run + __shfl_xor(l_run, 32);
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 v = {oacc[b][4 * g], oacc[b][4 * g + 1], oacc[b][4 * g + 2], oacc[b][4 * g + 3]};
+            *reinterpret_cast<f32x4*>(Om + (wave * 32 + r) * LD + 32 * b + 8 * g + 4 * h) = v;
+        }
+    if (h == 0) {
+        ml[(wave * 32 + r) * 2] = m_run;
+        ml[(wave * 32 + r) * 2 + 1] = l_tot;
+    }
+    __syncthreads();
+    // 256 threads: row = tid / 8, 8 threads per row each owning D/8 columns
+    const int row = tid >> 3, part = tid & 7;
+    float mw[4], lw[4], mstar = -__builtin_inff();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        mw[w] = ml[(w * 32 + row) * 2];
+        lw[w] = ml[(w * 32 + row) * 2 + 1];
+        mstar = fmaxf(mstar, mw[w]);
+    }
+    float lstar = 0.f, cw[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        cw[w] = (mw[w] == -__builtin_inff()) ? 0.f : fast_exp2(mw[w] - mstar);
+        lstar += cw[w] * lw[w];
+    }
+    const float inv = 1.f / lstar;
+    const int qrow = qb * 32 + row;
+    if (qrow < S) {
+        float* orow = O + base + (long)qrow * D;
+#pragma unroll
+        for (int c = 0; c < D / 32; ++c) {
+            const int col = 4 * (part + 8 * c);
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(Om + (w * 32 + row) * LD + col);
+                acc += v * cw[w];
+            }
+            *reinterpret_cast<f32x4*>(orow + col) = acc * inv;
+        }
+        if (part == 0) LSE[(long)bh * S + qrow] = mstar * FA2F_LN2 + __logf(lstar);
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256)
+fa2_fwd_f32_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                   float* __restrict__ O, float* __restrict__ LSE, int BH, int S) {
+    __shared__ __attribute__((aligned(16))) float smem[FwdLds<D>::FLOATS];
+    fwd_f32_body<D>(Q, K, V, O, LSE, BH, S, smem);
+}
+
+}  // namespace fa2f32
+
+#ifndef CUPY_INLINE_COMPILE
+namespace fa2 {
+
+template <int D>
+static hipError_t fwd_f32_dispatch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
+                                   hipStream_t stream) {
+    const long grid = (long)bh * ((S + 31) / 32);
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f32::fa2_fwd_f32_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, o, lse,
+                       bh, S);
+    return hipGetLastError();
+}
+
+hipError_t launch_forward_f32(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,
+                              int S, hipStream_t stream) {
+    if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
+    switch (D) {
+        case 32: return fwd_f32_dispatch<32>(q, k, v, o, lse, bh, S, stream);
+        case 64: return fwd_f32_dispatch<64>(q, k, v, o, lse, bh, S, stream);
+        case 128: return fwd_f32_dispatch<128>(q, k, v, o, lse, bh, S, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace fa2
+
+// Host API with the reference's semantics (kernel_fa2_optimized.cu:350-423).
+template <int head_dim>
+void host_flash_attention2_forward(const float* h_Q, const float* h_K, const float* h_V, float* h_O,
+                                   float* h_logsumexp, int batch_size, int seq_len, int num_heads, TimerManager* tm) {
+    const size_t n = (size_t)batch_size * num_heads * seq_len * head_dim;
+    const size_t nl = (size_t)batch_size * num_heads * seq_len;
+    float *dq, *dk, *dv, *dout, *dl;
+    HIP_CHECK(hipMalloc(&dq, n * sizeof(float)));
+    HIP_CHECK(hipMalloc(&dk, n * sizeof(float)));
+    HIP_CHECK(hipMalloc(&dv, n * sizeof(float)));
+    HIP_CHECK(hipMalloc(&dout, n * sizeof(float)));
+    HIP_CHECK(hipMalloc(&dl, nl * sizeof(float)));
+    HIP_CHECK(hipMemcpy(dq, h_Q, n * sizeof(float), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dk, h_K, n * sizeof(float), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dv, h_V, n * sizeof(float), hipMemcpyHostToDevice));
+    tm->Start();
+    HIP_CHECK(fa2::launch_forward_f32(head_dim, dq, dk, dv, dout, dl, batch_size * num_heads, seq_len, nullptr));
+    tm->Stop();
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy(h_O, dout, n * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(h_logsumexp, dl, nl * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipFree(dq));
+    HIP_CHECK(hipFree(dk));
+    HIP_CHECK(hipFree(dv));
+    HIP_CHECK(hipFree(dout));
+    HIP_CHECK(hipFree(dl));
+}
+template void host_flash_attention2_forward<32>(const float*, const float*, const float*, float*, float*, int, int,
+                                                int, TimerManager*);
+template void host_flash_attention2_forward<64>(const float*, const float*, const float*, float*, float*, int, int,
+                                                int, TimerManager*);
+template void host_flash_attention2_forward<128>(const float*, const float*, const float*, float*, float*, int, int,
+                                                 int, TimerManager*);
+#else
+// CuPy face: test_flash_attention2.py:113-126 compiles this file's text and
+// launches ((B*H*ceil(S/32),), (256,), (q,k,v,o,lse,B,H,S,D), shared_mem=29056).
+// Unlike the reference (which hard-wires 64, :438-442) head_dim is honoured.
+extern "C" __global__ void __launch_bounds__(256)
+flash_attention2_forward_kernel_wrapper(const float* query, const float* key, const float* value, float* output,
+                                        float* logsumexp, int batch_size, int num_heads, int seq_len, int head_dim) {
+    __shared__ __attribute__((aligned(16))) float smem[fa2f32::FwdLds<128>::FLOATS];
+    const int bh = batch_size * num_heads;
+    if (head_dim == 64)
+        fa2f32::fwd_f32_body<64>(query, key, value, output, logsumexp, bh, seq_len, smem);
+    else if (head_dim == 32)
+        fa2f32::fwd_f32_body<32>(query, key, value, output, logsumexp, bh, seq_len, smem);
+    else if (head_dim == 128)
+        fa2f32::fwd_f32_body<128>(query, key, value, output, logsumexp, bh, seq_len, smem);
+}
+#endif  // CUPY_INLINE_COMPILE

@@ -1,0 +1,345 @@
+// kernel_fa2_optimized_f16.cu -- FA2 forward, fp16-tile MFMA path, for MI355X (gfx950).
+//
+// Replaces detker/CUDA-Flash-Attention kernels/kernel_fa2_optimized_f16.cu
+// (flash_attention2_forward_kernel_fp16, :20-350; host launcher :353-430; CuPy
+// wrapper :432-448).  Same math: O = softmax(Q Kᵀ/√D) V, LSE = ln Σ exp + max,
+// fp32 tensors in HBM; the tiles live in fp16 and both contractions run on
+// v_mfma_f32_32x32x16_f16 with fp32 accumulation (the reference does scalar
+// fp32 FMAs on __half LDS tiles).
+//
+// Design:
+//   * one wave = 32 query rows; a workgroup = NW waves sharing 64-key K/V tiles;
+//   * S is computed transposed, Sᵀ = K·Qᵀ, so each lane owns one query and 32 of
+//     the tile's 64 keys in registers: the row max needs one cross-half
+//     exchange, the row sum none until the epilogue;
+//   * the Sᵀ accumulator, packed to fp16, IS the B operand of Oᵀ += Vᵀ·Pᵀ (no
+//     LDS round trip for P); Vᵀ comes from the row-major V tile through
+//     ds_read_b64_tr_b16;
+//   * Q is pre-scaled by log2(e)/√D so p = exp2(s - m) is one v_exp_f32;
+//   * K/V tiles: fp32 HBM -> registers (issued before the MFMAs of the previous
+//     tile) -> fp16 -> XOR-swizzled LDS, double-buffered, one barrier per tile;
+//   * blockIdx is remapped so all query blocks of one head share an XCD's L2.
+//
+// This file is self-contained device code so that it also compiles from source
+// text under hiprtc with -DCUPY_INLINE_COMPILE (the reference harness's
+// cp.RawModule path, test_flash_attention2.py:113-126), C++14 only.
+#ifndef CUPY_INLINE_COMPILE
+#include "f-attn2.cuh"
+#endif
+
+namespace fa2f16 {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+#define FA2_LOG2E 1.4426950408889634f
+#define FA2_LN2 0.6931471805599453f
+
+__device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// XOR swizzle of the 16-byte chunk index of LDS row r (fp16 rows of D halves).
+// Chosen by exhaustive search so that both access kinds used on a tile are
+// bank-conflict-free: ds_read_b128 row fragments (lane -> row) and
+// ds_read_b64_tr_b16 transposed fragments (4 rows x 32 cols per half-wave).
+template <int D> struct Swz;
+template <> struct Swz<32> {
+    static __device__ __forceinline__ int f(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) << 1); }
+};
+template <> struct Swz<64> {
+    static __device__ __forceinline__ int f(int r) {
+        return ((r >> 1) & 1) | (((r >> 2) & 1) << 1) | ((((r >> 1) ^ (r >> 3)) & 1) << 2);
+    }
+};
+template <> struct Swz<128> {
+    static __device__ __forceinline__ int f(int r) {
+        return (r & 1) | (((r >> 1) & 1) << 1) | (((r ^ (r >> 2)) & 1) << 2) | ((((r >> 1) ^ (r >> 3)) & 1) << 3);
+    }
+};
+
+// element offset (in halves) of (row, col) in a swizzled [rows][D] fp16 tile
+template <int D>
+__device__ __forceinline__ int tile_off(int row, int col) {
+    return row * D + (((col >> 3) ^ Swz<D>::f(row)) << 3) + (col & 7);
+}
+
+__device__ __forceinline__ f16x8 lds_row8(const _Float16* p) { return *reinterpret_cast<const f16x8*>(p); }
+
+__device__ __forceinline__ i16x4 lds_tr4(const _Float16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p));
+}
+
+__device__ __forceinline__ f16x8 cat4(i16x4 a, i16x4 b) {
+    i16x8 c = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(f16x8, c);
+}
+
+// A operand of a 32x32x16 MFMA whose k index runs over rows of a row-major tile
+// in the order an accumulator-as-B-operand imposes (guide: "accumulator tile as
+// the next MFMA's operand"): lane l gets column c0 + (l & 31) of rows
+// r0 + 4*(l>>5) + {0..3} and r0 + 8 + 4*(l>>5) + {0..3}.
+template <int D>
+__device__ __forceinline__ f16x8 tr_operand(const _Float16* tile, int r0, int c0, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    const int row = r0 + 4 * (g >> 1) + (i >> 2);
+    const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+    return cat4(lds_tr4(tile + tile_off<D>(row, col)), lds_tr4(tile + tile_off<D>(row + 8, col)));
+}
+
+__device__ __forceinline__ f16x8 to_f16x8(f32x4 a, f32x4 b, float s) {
+    f16x8 r;
+    r[0] = (_Float16)(a[0] * s); r[1] = (_Float16)(a[1] * s); r[2] = (_Float16)(a[2] * s); r[3] = (_Float16)(a[3] * s);
+    r[4] = (_Float16)(b[0] * s); r[5] = (_Float16)(b[1] * s); r[6] = (_Float16)(b[2] * s); r[7] = (_Float16)(b[3] * s);
+    return r;
+}
+
+// Bijective XCD-aware remap (guide T1): consecutive logical blocks land on one XCD.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int q = nwg >> 3, rr = nwg & 7, xcd = orig & 7, idx = orig >> 3;
+    return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+}
+
+// Register-staged tile loader: ROWS x D fp32 rows [row0, row0+ROWS) of a [S][D]
+// tensor -> fp16 swizzled LDS.  Rows >= S load zeros.  CPT chunks (8 floats) per thread.
+template <int D, int ROWS, int NT>
+struct TileStager {
+    static constexpr int CPR = D / 8;
+    static constexpr int CHUNKS = ROWS * CPR;
+    static constexpr int CPT = (CHUNKS + NT - 1) / NT;
+    f32x4 r[CPT][2];
+
+    __device__ __forceinline__ void load(const float* __restrict__ src, int row0, int S, int tid) {
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int x = tid + c * NT;
+            const int row = x / CPR, ch = x % CPR;
+            if ((CHUNKS % NT == 0 || x < CHUNKS) && row0 + row < S) {
+                const f32x4* p = reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * D + ch * 8);
+                r[c][0] = p[0];
+                r[c][1] = p[1];
+            } else {
+                r[c][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                r[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    }
+    __device__ __forceinline__ void store(_Float16* tile, int tid, float scale) const {
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int x = tid + c * NT;
+            if (CHUNKS % NT == 0 || x < CHUNKS) {
+                const int row = x / CPR, ch = x % CPR;
+                *reinterpret_cast<f16x8*>(tile + row * D + ((ch ^ Swz<D>::f(row)) << 3)) =
+                    to_f16x8(r[c][0], r[c][1], scale);
+            }
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+// Grid: BH * ceil(S / (32*NW)) workgroups of 64*NW threads.
+template <int D, int NW>
+__global__ void __launch_bounds__(64 * NW)
+fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                   float* __restrict__ O, float* __restrict__ LSE, int S) {
+    constexpr int KT = 64;  // keys per tile
+    constexpr int NT = 64 * NW;
+    constexpr int TILE = KT * D;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int nqb = (S + 32 * NW - 1) / (32 * NW);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = bid / nqb, qb = bid - bh * nqb;
+    const long base = (long)bh * S * D;
+    const int q = qb * 32 * NW + wave * 32 + r;
+    const float qscale = FA2_LOG2E / __builtin_sqrtf((float)D);
+
+    // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16t + 8h + 0..7]
+    f16x8 qf[D / 16];
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+        if (q < S) {
+            const f32x4* p = reinterpret_cast<const f32x4*>(Q + base + (long)q * D + 16 * t + 8 * h);
+            qf[t] = to_f16x8(p[0], p[1], qscale);
+        } else {
+            qf[t] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    f32x16 oacc[D / 32];
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[b][i] = 0.f;
+    float m = -__builtin_inff(), l = 0.f;
+
+    const int ntiles = (S + KT - 1) / KT;
+    TileStager<D, KT, NT> ks, vs;
+    ks.load(K + base, 0, S, tid);
+    vs.load(V + base, 0, S, tid);
+    ks.store(smem, tid, 1.f);
+    vs.store(smem + TILE, tid, 1.f);
+    __syncthreads();
+
+    for (int j = 0; j < ntiles; ++j) {
+        const _Float16* Ks = smem + (j & 1) * 2 * TILE;
+        const _Float16* Vs = Ks + TILE;
+        const bool more = j + 1 < ntiles;
+        if (more) {
+            ks.load(K + base, (j + 1) * KT, S, tid);
+            vs.load(V + base, (j + 1) * KT, S, tid);
+        }
+
+        // S^T (64 keys x 32 queries) as two 32x32 blocks
+        f32x16 sacc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
+#pragma unroll
+            for (int t = 0; t < D / 16; ++t)
+                sacc[kb] = mfma(lds_row8(Ks + tile_off<D>(kb * 32 + r, 16 * t + 8 * h)), qf[t], sacc[kb]);
+        }
+        const int k0 = j * KT;
+        if (k0 + KT > S) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[kb][i] = -__builtin_inff();
+        }
+        // online softmax (row = this lane's query; the two half-waves hold 32 keys each)
+        float mx = sacc[0][0];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kb][i]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mnew = fmaxf(m, mx);
+        if (__any(mnew > m)) {
+            const float alpha = fast_exp2(m - mnew);
+            l *= alpha;
+#pragma unroll
+            for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) oacc[b][i] *= alpha;
+        }
+        m = mnew;
+        f16x8 pf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float p = fast_exp2(sacc[kb][i] - m);
+                l += p;
+                pf[kb][i >> 3][i & 7] = (_Float16)p;
+            }
+        // O^T += V^T P^T
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    oacc[b] = mfma(tr_operand<D>(Vs, kb * 32 + 16 * s, 32 * b, lane), pf[kb][s], oacc[b]);
+
+        if (more) {
+            _Float16* nxt = smem + ((j + 1) & 1) * 2 * TILE;
+            ks.store(nxt, tid, 1.f);
+            vs.store(nxt + TILE, tid, 1.f);
+        }
+        __syncthreads();
+    }
+
+    const float lt = l + __shfl_xor(l, 32);
+    const float inv = 1.f / lt;
+    if (q < S) {
+        float* orow = O + base + (long)q * D;
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 v = {oacc[b][4 * g] * inv, oacc[b][4 * g + 1] * inv, oacc[b][4 * g + 2] * inv,
+                           oacc[b][4 * g + 3] * inv};
+                *reinterpret_cast<f32x4*>(orow + 32 * b + 8 * g + 4 * h) = v;
+            }
+        if (h == 0) LSE[(long)bh * S + q] = m * FA2_LN2 + __logf(lt);
+    }
+}
+
+}  // namespace fa2f16
+
+#ifndef CUPY_INLINE_COMPILE
+namespace fa2 {
+
+template <int D>
+static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
+                                   hipStream_t stream) {
+    constexpr int NW = 4;
+    const int nqb = (S + 32 * NW - 1) / (32 * NW);
+    const long grid = (long)bh * nqb;
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k, v, o,
+                       lse, S);
+    return hipGetLastError();
+}
+
+hipError_t launch_forward_f16(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,
+                              int S, hipStream_t stream) {
+    if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
+    switch (D) {
+        case 32: return fwd_f16_dispatch<32>(q, k, v, o, lse, bh, S, stream);
+        case 64: return fwd_f16_dispatch<64>(q, k, v, o, lse, bh, S, stream);
+        case 128: return fwd_f16_dispatch<128>(q, k, v, o, lse, bh, S, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace fa2
+
+// Host API with the reference's semantics (kernel_fa2_optimized_f16.cu:353-430):
+// host buffers in, device alloc + H2D, timed launch, D2H, free.
+template <int head_dim>
+void host_flash_attention2_forward_fp16(const float* h_Q, const float* h_K, const float* h_V, float* h_O,
+                                        float* h_logsumexp, int batch_size, int seq_len, int num_heads,
+                                        TimerManager* tm) {
+    const size_t n = (size_t)batch_size * num_heads * seq_len * head_dim;
+    const size_t nl = (size_t)batch_size * num_heads * seq_len;
+    float *dq, *dk, *dv, *dout, *dl;
+    HIP_CHECK(hipMalloc(&dq, n * sizeof(float)));
+    HIP_CHECK(hipMalloc(&dk, n * sizeof(float)));
+    HIP_CHECK(hipMalloc(&dv, n * sizeof(float)));
+    HIP_CHECK(hipMalloc(&dout, n * sizeof(float)));
+    HIP_CHECK(hipMalloc(&dl, nl * sizeof(float)));
+    HIP_CHECK(hipMemcpy(dq, h_Q, n * sizeof(float), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dk, h_K, n * sizeof(float), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dv, h_V, n * sizeof(float), hipMemcpyHostToDevice));
+    tm->Start();
+    HIP_CHECK(fa2::launch_forward_f16(head_dim, dq, dk, dv, dout, dl, batch_size * num_heads, seq_len, nullptr));
+    tm->Stop();
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipMemcpy(h_O, dout, n * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(h_logsumexp, dl, nl * sizeof(float), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipFree(dq));
+    HIP_CHECK(hipFree(dk));
+    HIP_CHECK(hipFree(dv));
+    HIP_CHECK(hipFree(dout));
+    HIP_CHECK(hipFree(dl));
+}
+template void host_flash_attention2_forward_fp16<32>(const float*, const float*, const float*, float*, float*, int,
+                                                     int, int, TimerManager*);
+template void host_flash_attention2_forward_fp16<64>(const float*, const float*, const float*, float*, float*, int,
+                                                     int, int, TimerManager*);
+template void host_flash_attention2_forward_fp16<128>(const float*, const float*, const float*, float*, float*, int,
+                                                      int, int, TimerManager*);
+#endif  // CUPY_INLINE_COMPILE

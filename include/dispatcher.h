@@ -1,0 +1,147 @@
+// dispatcher.h -- runtime head_dim -> template<HEAD_DIM>, then method x precision x mode.
+//
+// Same entry point and behaviour as detker/CUDA-Flash-Attention
+// include/dispatcher.h:220-246 (RunFlashAttention) with its
+// FlashAttentionDispatcher (:11-104) and RuntimeDimDispatcher (:107-141):
+// head_dim is matched by doubling from 32 (here up to 128); forward_backward runs
+// the forward then the backward, O and LSE passing through host memory exactly
+// as there (:91-104).  Only FlashAttention2 is built (SURVEY §2 marks the naive /
+// FA1 baselines out of scope); asking for them exits(1) with a message, as the
+// reference does for its own unsupported combinations (:30-47, :74-83).
+//
+// FA2_NUM_DEVICES=N (environment) shards the B*H heads over N GPUs through the C
+// ABI's host API (fa2_amd.h), one host thread per device, no collective.
+#pragma once
+
+#include <cstdio>
+#include <cstdlib>
+#include <utility>
+
+#include "enum_types.h"
+#include "f-attn2.cuh"
+#include "fa2_amd.h"
+#include "timer.h"
+
+inline int fa2_env_devices() {
+    const char* s = getenv("FA2_NUM_DEVICES");
+    const int n = s ? atoi(s) : 1;
+    return n < 1 ? 1 : n;
+}
+
+template <int HEAD_DIM>
+struct FlashAttentionDispatcher {
+    static void require_fa2(ComputeType m) {
+        if (m != ComputeType::FlashAttention2) {
+            fprintf(stderr, "Error: only the fa2 method is part of this build (naive/fa1 are reference baselines)\n");
+            exit(EXIT_FAILURE);
+        }
+    }
+    static void sharded(int rc, float ms, TimerManager* tm) {
+        if (rc) {
+            fprintf(stderr, "Error: %s\n", fa2_last_error());
+            exit(EXIT_FAILURE);
+        }
+        tm->AddMillis(ms);  // kernel time = max over devices
+    }
+
+    static void dispatch_forward(const float* Q, const float* K, const float* V, float* O, float* lse, int B, int H,
+                                 int S, ComputeDataType prec, ComputeType method, TimerManager* tm) {
+        require_fa2(method);
+        const int ndev = fa2_env_devices();
+        if (ndev > 1) {
+            float ms = 0.f;
+            const int rc = fa2_forward_host(Q, K, V, O, lse, B, H, S, HEAD_DIM,
+                                            prec == ComputeDataType::FP16 ? FA2_FP16 : FA2_FP32, ndev, &ms);
+            sharded(rc, ms, tm);
+            return;
+        }
+        if (prec == ComputeDataType::FP16) {
+            printf("Running Flash Attention 2 Forward (HEAD_DIM=%d) with FP16 tiles (MFMA)...\n", HEAD_DIM);
+            host_flash_attention2_forward_fp16<HEAD_DIM>(Q, K, V, O, lse, B, S, H, tm);
+        } else {
+            printf("Running Flash Attention 2 Forward (HEAD_DIM=%d)...\n", HEAD_DIM);
+            host_flash_attention2_forward<HEAD_DIM>(Q, K, V, O, lse, B, S, H, tm);
+        }
+    }
+
+    static void dispatch_backward(const float* Q, const float* K, const float* V, const float* O, const float* dO,
+                                  const float* lse, float* dQ, float* dK, float* dV, int B, int H, int S,
+                                  ComputeDataType prec, ComputeType method, TimerManager* tm) {
+        require_fa2(method);
+        const int ndev = fa2_env_devices();
+        if (ndev > 1) {
+            float ms = 0.f;
+            const int rc = fa2_backward_host(Q, K, V, O, dO, lse, dQ, dK, dV, B, H, S, HEAD_DIM,
+                                             prec == ComputeDataType::FP16 ? FA2_FP16 : FA2_FP32, ndev, &ms);
+            sharded(rc, ms, tm);
+            return;
+        }
+        if (prec == ComputeDataType::FP16) {
+            printf("Running Flash Attention 2 Backward (HEAD_DIM=%d) with FP16 tiles (MFMA)...\n", HEAD_DIM);
+            host_flash_attention2_backward_fp16<HEAD_DIM>(Q, K, V, O, dO, lse, dQ, dK, dV, B, S, H, tm);
+        } else {
+            printf("Running Flash Attention 2 Backward (HEAD_DIM=%d)...\n", HEAD_DIM);
+            host_flash_attention2_backward<HEAD_DIM>(Q, K, V, O, dO, lse, dQ, dK, dV, B, S, H, tm);
+        }
+    }
+
+    static void dispatch_forward_backward(const float* Q, const float* K, const float* V, float* O, float* lse,
+                                          const float* dO, float* dQ, float* dK, float* dV, int B, int H, int S,
+                                          ComputeDataType prec, ComputeType method, TimerManager* tm) {
+        printf("Running Forward+Backward Pass (HEAD_DIM=%d)...\n", HEAD_DIM);
+        dispatch_forward(Q, K, V, O, lse, B, H, S, prec, method, tm);
+        dispatch_backward(Q, K, V, O, dO, lse, dQ, dK, dV, B, H, S, prec, method, tm);
+    }
+};
+
+template <int CurrentD, int MaxD>
+struct RuntimeDimDispatcher {
+    template <typename F>
+    static void dispatch(int head_dim, F&& f) {
+        if (head_dim == CurrentD) f.template operator()<CurrentD>();
+        else RuntimeDimDispatcher<CurrentD * 2, MaxD>::dispatch(head_dim, std::forward<F>(f));
+    }
+};
+template <int MaxD>
+struct RuntimeDimDispatcher<MaxD, MaxD> {
+    template <typename F>
+    static void dispatch(int head_dim, F&& f) {
+        if (head_dim == MaxD) {
+            f.template operator()<MaxD>();
+        } else {
+            fprintf(stderr, "Error: Unsupported head dimension %d\n", head_dim);
+            exit(EXIT_FAILURE);
+        }
+    }
+};
+
+struct FlashAttentionLaunch {
+    const float *Q, *K, *V;
+    float *O, *lse;
+    const float* dO;
+    float *dQ, *dK, *dV;
+    int B, H, S;
+    ComputeDataType prec;
+    ComputeType method;
+    ModeType mode;
+    TimerManager* tm;
+    template <int D>
+    void operator()() const {
+        using FD = FlashAttentionDispatcher<D>;
+        if (mode == ModeType::Forward) FD::dispatch_forward(Q, K, V, O, lse, B, H, S, prec, method, tm);
+        else if (mode == ModeType::Backward)
+            FD::dispatch_backward(Q, K, V, O, dO, lse, dQ, dK, dV, B, H, S, prec, method, tm);
+        else FD::dispatch_forward_backward(Q, K, V, O, lse, dO, dQ, dK, dV, B, H, S, prec, method, tm);
+    }
+};
+
+inline void RunFlashAttention(const float* Q, const float* K, const float* V, float* O, float* logsumexp,
+                              const float* dO, float* dQ, float* dK, float* dV, int batch_size, int num_heads,
+                              int seq_len, int head_dim, ComputeDataType compute_data_type, ComputeType compute_method,
+                              ModeType mode, TimerManager* tm) {
+    static constexpr int MIN_HEAD_DIM = 32;
+    static constexpr int MAX_HEAD_DIM = 128;
+    FlashAttentionLaunch l{Q, K, V, O, logsumexp, dO, dQ, dK, dV, batch_size, num_heads, seq_len,
+                           compute_data_type, compute_method, mode, tm};
+    RuntimeDimDispatcher<MIN_HEAD_DIM, MAX_HEAD_DIM>::dispatch(head_dim, l);
+}

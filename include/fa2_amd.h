@@ -1,0 +1,99 @@
+/*
+ * fa2_amd.h -- C ABI of the MI355X-native FA2 forward+backward (libfa2amd.so).
+ *
+ * The drop-in boundary for detker/CUDA-Flash-Attention's hot path.  Plain
+ * pointers and sizes, no C++ or torch types, so any FFI (ctypes, cgo, JNI,
+ * N-API) can bind it; see INTEGRATION.md for the bindings.  Every entry point
+ * returns 0 on success or a negative FA2_E* code; fa2_last_error() returns the
+ * calling thread's last message.  Nothing here calls exit().
+ *
+ * Tensor layout everywhere (as in the reference): fp32, [B,H,S,D] row-major for
+ * Q, K, V, O, dO, dQ, dK, dV; [B,H,S] for logsumexp (natural log) and delta.
+ * head_dim D must be 32, 64 or 128 (the reference instantiates 32 and 64,
+ * kernels/kernel_fa2_optimized.cu:424-426; 128 is BASELINE config C4's).
+ *
+ * `precision` mirrors the reference's ComputeDataType (include/enum_types.h:15-18):
+ *   FA2_FP32 -- fp32 tiles, exact-fp32 MFMA (the reference's default .cu files);
+ *   FA2_FP16 -- fp16 tiles, MFMA f16 -> fp32 accumulate (the _f16.cu files).
+ */
+#ifndef FA2_AMD_H
+#define FA2_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { FA2_FP16 = 0, FA2_FP32 = 1 };
+
+enum {
+    FA2_OK = 0,
+    FA2_E_INVALID = -1,   /* bad shape, head_dim, precision or null pointer */
+    FA2_E_DEVICE = -2,    /* HIP runtime / launch failure (see fa2_last_error) */
+    FA2_E_NOMEM = -3      /* device allocation failed */
+};
+
+/* ---------------------------------------------------------------------------
+ * Device-pointer API.  Inputs already resident in HBM; launches are async on
+ * `stream` (a hipStream_t, NULL = default stream); nothing allocates or
+ * synchronises, so calls are hipGraph-capturable.
+ * ------------------------------------------------------------------------- */
+
+/* Forward: O, LSE.  Replaces the device half of host_flash_attention2_forward[_fp16]
+ * (kernels/f-attn2.cuh:13-24 / :43-54) and the CuPy launch of
+ * flash_attention2_forward_kernel_wrapper (kernel_fa2_optimized.cu:428-444). */
+int fa2_forward(const float* q, const float* k, const float* v, float* o, float* lse, int batch, int heads, int seq,
+                int head_dim, int precision, void* stream);
+
+/* Δ = rowsum(dO ∘ O).  Replaces D_computation_reduction_kernel(_wrapper)
+ * (f-attn2-backward.cu:341-380, :515-528); the output pointer comes last there,
+ * first-class here. */
+int fa2_delta(const float* dout, const float* o, float* delta, int batch, int heads, int seq, int head_dim,
+              void* stream);
+
+/* Backward: dQ, dK, dV (fully overwritten; no pre-zeroing needed).  `delta` is
+ * [B,H,S] scratch that receives Δ.  Replaces the device half of
+ * host_flash_attention2_backward[_fp16] (kernels/f-attn2.cuh:26-41 / :56-71) and
+ * the CuPy launches of D_computation_reduction_kernel_wrapper +
+ * flash_attention2_backward_kernel_wrapper (f-attn2-backward.cu:491-528). */
+int fa2_backward(const float* q, const float* k, const float* v, const float* o, const float* dout,
+                 const float* lse, float* delta, float* dq, float* dk, float* dv, int batch, int heads, int seq,
+                 int head_dim, int precision, void* stream);
+
+/* The two MFMA kernels of the fp16 backward, separately (profiling/bench hooks;
+ * fa2_backward with FA2_FP16 = fa2_delta + these two). */
+int fa2_backward_dkdv(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                      const float* delta, float* dk, float* dv, int batch, int heads, int seq, int head_dim,
+                      void* stream);
+int fa2_backward_dq(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                    const float* delta, float* dq, int batch, int heads, int seq, int head_dim, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Host-pointer API: the reference host functions' semantics
+ * (kernel_fa2_optimized.cu:350-423, f-attn2-backward.cu:384-485): host buffers
+ * in and out, device alloc + H2D + timed kernels + D2H + free, synchronous.
+ * *kernel_ms (may be NULL) receives the hipEvent-timed kernel milliseconds
+ * (what TimerManager accumulates; copies excluded).
+ *
+ * num_devices > 1 shards the B*H heads contiguously over devices 0..n-1, one
+ * host thread per device, each copying only its slice (no
+ * collective).  *kernel_ms is then the max over devices.
+ * ------------------------------------------------------------------------- */
+int fa2_forward_host(const float* q, const float* k, const float* v, float* o, float* lse, int batch, int heads,
+                     int seq, int head_dim, int precision, int num_devices, float* kernel_ms);
+int fa2_backward_host(const float* q, const float* k, const float* v, const float* o, const float* dout,
+                      const float* lse, float* dq, float* dk, float* dv, int batch, int heads, int seq, int head_dim,
+                      int precision, int num_devices, float* kernel_ms);
+
+/* Shard helper shared by the C++ and Python drivers: heads [*first, *first+*count)
+ * of `total_heads` belong to shard `index` of `shards` (contiguous, balanced). */
+int fa2_shard_range(int total_heads, int shards, int index, int* first, int* count);
+
+const char* fa2_last_error(void);
+int fa2_version(void); /* MAJOR*10000 + MINOR*100 + PATCH */
+int fa2_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FA2_AMD_H */

@@ -1,0 +1,98 @@
+"""CPU-only checks of the boundary: the C-ABI library loads and exports every
+symbol include/fa2_amd.h declares, argument validation needs no GPU, the shard
+rule, the CLI's argv/dir contract, and the hiprtc (CuPy-face) compile of the
+reference-named kernel files.  No compute call touches a device here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import fa2amd
+from fa2amd import rawmodule
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fa2_amd.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(fa2_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = fa2amd.lib()
+    declared = header_functions()
+    assert len(declared) >= 10
+    for name in declared:
+        assert hasattr(L, name), name
+    assert sorted(fa2amd.C_SYMBOLS) == declared
+
+
+def test_version():
+    assert fa2amd.version() == 10000
+
+
+def test_invalid_arguments_rejected_without_device():
+    L = fa2amd.lib()
+    null = ctypes.c_void_p(0)
+    one = ctypes.c_void_p(16)
+    # bad head_dim
+    rc = L.fa2_forward(one, one, one, one, one, 1, 1, 8, 48, fa2amd.FA2_FP16, null)
+    assert rc == -1 and b"head_dim" in L.fa2_last_error()
+    # bad precision
+    rc = L.fa2_forward(one, one, one, one, one, 1, 1, 8, 64, 7, null)
+    assert rc == -1 and b"precision" in L.fa2_last_error()
+    # null pointer
+    rc = L.fa2_backward(one, one, one, one, one, one, one, one, null, one, 1, 1, 8, 64, fa2amd.FA2_FP32, null)
+    assert rc == -1 and b"null" in L.fa2_last_error()
+    # non-positive sizes
+    assert L.fa2_delta(one, one, one, 0, 1, 8, 64, null) == -1
+
+
+@pytest.mark.parametrize("total,shards", [(16, 1), (16, 2), (1024, 8), (7, 3), (3, 8), (64, 4)])
+def test_shard_range_c_and_python_agree(total, shards):
+    L = fa2amd.lib()
+    covered = []
+    for i in range(shards):
+        f, c = ctypes.c_int(), ctypes.c_int()
+        assert L.fa2_shard_range(total, shards, i, ctypes.byref(f), ctypes.byref(c)) == 0
+        assert (f.value, c.value) == fa2amd.shard_range(total, shards, i)
+        covered.extend(range(f.value, f.value + c.value))
+    assert covered == list(range(total))  # contiguous, disjoint, complete
+
+
+def test_python_api_refuses_cpu_tensors():
+    import torch
+    q = torch.zeros(1, 1, 8, 64)
+    with pytest.raises(fa2amd.FA2Error):
+        fa2amd.forward(q, q, q)
+
+
+@pytest.mark.parametrize("argv,needle", [
+    ([], "USAGE"),
+    (["fa3", "forward", "fp32", "x/B1_H1_S8_D64"], "USAGE"),
+    (["fa2", "both", "fp32", "x/B1_H1_S8_D64"], "USAGE"),
+    (["fa2", "forward", "bf16", "x/B1_H1_S8_D64"], "USAGE"),
+    (["fa2", "forward", "fp32", "x/not_a_shape"], "sscanf"),
+])
+def test_cli_argv_contract(argv, needle):
+    r = subprocess.run([fa2amd.CLI_PATH] + argv, capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert needle in r.stderr
+
+
+@pytest.mark.parametrize("fname,symbols", [
+    ("kernel_fa2_optimized.cu", ["flash_attention2_forward_kernel_wrapper"]),
+    ("f-attn2-backward.cu", ["D_computation_reduction_kernel_wrapper", "flash_attention2_backward_kernel_wrapper"]),
+])
+def test_cupy_face_compiles_under_hiprtc(fname, symbols):
+    """test_flash_attention2.py:113-145 compiles these files' text with
+    ('-std=c++14', '-DCUPY_INLINE_COMPILE'); the same must work here."""
+    co = rawmodule.compile_source(rawmodule.load_kernel_source(fname))
+    exported = rawmodule.exported_kernels(co)
+    for s in symbols:
+        assert s in exported
