@@ -26,17 +26,32 @@ _rtc = None
 _hip = None
 
 
+def _libdir():
+    """Directory of the HIP runtime to bind.  Once torch is imported its bundled
+    libamdhip64 / libhsa-runtime64 are the process's HIP runtime; a second copy
+    from /opt/rocm would not resolve against them (undefined hsa_* symbols), so
+    bind torch's copies then, and /opt/rocm's otherwise."""
+    import sys
+
+    t = sys.modules.get("torch")
+    if t is not None:
+        d = os.path.join(os.path.dirname(t.__file__), "lib")
+        if os.path.exists(os.path.join(d, "libamdhip64.so")):
+            return d
+    return os.path.join(ROCM, "lib")
+
+
 def _hiprtc():
     global _rtc
     if _rtc is None:
-        _rtc = ctypes.CDLL(os.path.join(ROCM, "lib", "libhiprtc.so"))
+        _rtc = ctypes.CDLL(os.path.join(_libdir(), "libhiprtc.so"))
     return _rtc
 
 
 def _hipapi():
     global _hip
     if _hip is None:
-        _hip = ctypes.CDLL(os.path.join(ROCM, "lib", "libamdhip64.so"))
+        _hip = ctypes.CDLL(os.path.join(_libdir(), "libamdhip64.so"))
     return _hip
 
 
@@ -87,14 +102,43 @@ def exported_kernels(code_object: bytes):
     return sorted({m.decode() for m in re.findall(rb"([A-Za-z_][A-Za-z0-9_]*)\.kd\x00", code_object)})
 
 
+MAX_LDS_BYTES = 160 * 1024  # per workgroup on gfx950 (MI355X_MICROARCH.md, LDS per CU)
+
+
+def static_lds_bytes(code_object: bytes) -> dict:
+    """{kernel: group_segment_fixed_size} from the code object's AMDGPU metadata note."""
+    import subprocess
+    import tempfile
+
+    readelf = os.path.join(ROCM, "lib", "llvm", "bin", "llvm-readelf")
+    with tempfile.NamedTemporaryFile(suffix=".co") as f:
+        f.write(code_object)
+        f.flush()
+        out = subprocess.run([readelf, "--notes", f.name], capture_output=True, text=True, check=True).stdout
+    sizes, pending = {}, None
+    for line in out.splitlines():
+        line = line.strip()
+        if line.startswith(".group_segment_fixed_size:"):
+            pending = int(line.split(":")[1])
+        elif line.startswith(".name:") and pending is not None:
+            sizes[line.split(":", 1)[1].strip()] = pending
+            pending = None
+    return sizes
+
+
 class RawFunction:
-    def __init__(self, fn):
+    def __init__(self, fn, name="", static_lds=0):
         self._fn = fn
+        self.name = name
+        self.static_lds = static_lds
 
     def __call__(self, grid, block, args, shared_mem=0, stream=None):
         """Launch like ``cupy.RawKernel.__call__``: tensors by data pointer, ints as int64."""
         import torch
 
+        if self.static_lds + shared_mem > MAX_LDS_BYTES:
+            raise HipError(f"{self.name}: {self.static_lds} B static + {shared_mem} B dynamic LDS exceeds "
+                           f"the {MAX_LDS_BYTES} B a workgroup may own")
         storage = []
         for a in args:
             if isinstance(a, torch.Tensor):
@@ -125,13 +169,14 @@ class RawModule:
         missing = [n for n in name_expressions if n not in exported_kernels(self.code_object)]
         if missing:
             raise HipError(f"symbols not exported by the module: {missing}")
+        self.static_lds = static_lds_bytes(self.code_object)
         self._mod = ctypes.c_void_p()
         _chk(_hipapi().hipModuleLoadData(ctypes.byref(self._mod), self.code_object), "hipModuleLoadData")
 
     def get_function(self, name: str) -> RawFunction:
         fn = ctypes.c_void_p()
         _chk(_hipapi().hipModuleGetFunction(ctypes.byref(fn), self._mod, name.encode()), "hipModuleGetFunction")
-        return RawFunction(fn)
+        return RawFunction(fn, name, self.static_lds.get(name, 0))
 
 
 def load_kernel_source(filename: str) -> str:

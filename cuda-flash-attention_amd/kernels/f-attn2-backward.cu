@@ -94,13 +94,18 @@ __global__ void __launch_bounds__(256) fa2_delta_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------
 // backward body: 32 keys per workgroup of 4 waves, grid = BH * ceil(S/32)
 // ---------------------------------------------------------------------------
+// LDS of the backward body in two regions: TR = the Q/dO super-tile (also the
+// dK/dV merge buffer) + the super-tile's lse2/delta rows; KD = this workgroup's
+// K and V tiles + the per-wave dS transpose scratch.
 template <int D> struct BwdLds {
     static constexpr int LD = D + 4;
-    static constexpr int T = 128 * LD;        // Q / dO super-tile (also the dK/dV merge buffer)
-    static constexpr int KV = 32 * LD;        // K and V tiles of this workgroup
-    static constexpr int DS = 4 * 32 * 33;    // per-wave dS transpose scratch
-    static constexpr int ROWS = 2 * 128;      // lse2 and delta of the super-tile
-    static constexpr int FLOATS = T + 2 * KV + DS + ROWS;
+    static constexpr int T = 128 * LD;
+    static constexpr int ROWS = 2 * 128;
+    static constexpr int KV = 32 * LD;
+    static constexpr int DS = 4 * 32 * 33;
+    static constexpr int TR = T + ROWS;
+    static constexpr int KD = 2 * KV + DS;
+    static constexpr int FLOATS = TR + KD;
 };
 
 template <int D>
@@ -108,15 +113,15 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
                                              const float* __restrict__ V, const float* __restrict__ dO,
                                              const float* __restrict__ LSE, const float* __restrict__ Delta,
                                              float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV,
-                                             int BH, int S, float* smem) {
+                                             int BH, int S, float* tr_lds, float* kd_lds) {
     constexpr int LD = D + 4;
     constexpr int QS = 128;
-    float* T = smem;
-    float* Kt = T + BwdLds<D>::T;
+    float* T = tr_lds;
+    float* lse2 = T + BwdLds<D>::T;
+    float* del = lse2 + QS;
+    float* Kt = kd_lds;
     float* Vt = Kt + BwdLds<D>::KV;
     float* Ds = Vt + BwdLds<D>::KV;
-    float* lse2 = Ds + BwdLds<D>::DS;
-    float* del = lse2 + QS;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int nkb = (S + 31) / 32;
@@ -255,7 +260,7 @@ fa2_bwd_f32_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                    const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
                    float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV, int BH, int S) {
     __shared__ __attribute__((aligned(16))) float smem[BwdLds<D>::FLOATS];
-    bwd_f32_body<D>(Q, K, V, dO, LSE, Delta, dQ, dK, dV, BH, S, smem);
+    bwd_f32_body<D>(Q, K, V, dO, LSE, Delta, dQ, dK, dV, BH, S, smem, smem + BwdLds<D>::TR);
 }
 
 }  // namespace fa2f32b
@@ -343,23 +348,41 @@ FA2_INST_BWD32(64)
 FA2_INST_BWD32(128)
 #else
 // CuPy face (test_flash_attention2.py:132-141, 499-535).  dQ/dK/dV arrive zeroed.
+// LDS: the launch adds the harness's dynamic bytes ((32D + 4*32D + 32 + 32*32)*4,
+// 45 184 at D=64, :522-527) to this kernel's static bytes, and the sum must stay
+// within the 160 KiB a workgroup may own.  Static LDS is therefore sized for
+// D <= 64 (70 KB); at D = 128 the Q/dO super-tile moves into the dynamic region
+// (86 KB provided there).  The dispatch packet's group_segment_size (static +
+// dynamic) is checked first, so an undersized launch writes nothing instead of
+// running past its LDS.
+__device__ __forceinline__ unsigned fa2_group_segment_bytes() {
+    // hsa_kernel_dispatch_packet_t: group_segment_size is the u32 at byte offset 28
+    const unsigned char* pkt = (const unsigned char*)__builtin_amdgcn_dispatch_ptr();
+    return *(const unsigned*)(pkt + 28);
+}
+
 extern "C" __global__ void __launch_bounds__(256)
 flash_attention2_backward_kernel_wrapper(const float* query, const float* key, const float* value,
                                          const float* output, const float* d_output, const float* logsumexp,
                                          const float* d, float* d_query, float* d_key, float* d_value,
                                          int batch_size, int num_heads, int seq_len, int head_dim) {
-    __shared__ __attribute__((aligned(16))) float smem[fa2f32b::BwdLds<128>::FLOATS];
+    __shared__ __attribute__((aligned(16))) float smem[fa2f32b::BwdLds<64>::FLOATS];
+    extern __shared__ __attribute__((aligned(16))) float dyn[];
     (void)output;
     const int bh = batch_size * num_heads;
-    if (head_dim == 64)
+    const unsigned have = fa2_group_segment_bytes();
+    if (head_dim == 64) {
         fa2f32b::bwd_f32_body<64>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
-                                  smem);
-    else if (head_dim == 32)
+                                  smem, smem + fa2f32b::BwdLds<64>::TR);
+    } else if (head_dim == 32) {
         fa2f32b::bwd_f32_body<32>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
-                                  smem);
-    else if (head_dim == 128)
+                                  smem, smem + fa2f32b::BwdLds<32>::TR);
+    } else if (head_dim == 128) {
+        if (have < sizeof(smem) + 4u * fa2f32b::BwdLds<128>::TR) return;
+        static_assert(fa2f32b::BwdLds<128>::KD <= fa2f32b::BwdLds<64>::FLOATS, "KD region must fit the static LDS");
         fa2f32b::bwd_f32_body<128>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
-                                   smem);
+                                   dyn, smem);
+    }
 }
 
 // Note the output pointer comes last, as in the reference (f-attn2-backward.cu:515-528).

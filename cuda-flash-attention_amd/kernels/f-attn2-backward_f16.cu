@@ -70,13 +70,6 @@ __device__ __forceinline__ f16x8 cat4(i16x4 a, i16x4 b) {
     i16x8 c = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(f16x8, c);
 }
-template <int D>
-__device__ __forceinline__ f16x8 tr_operand(const _Float16* tile, int r0, int c0, int lane) {
-    const int g = lane >> 4, i = lane & 15;
-    const int row = r0 + 4 * (g >> 1) + (i >> 2);
-    const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
-    return cat4(lds_tr4(tile + tile_off<D>(row, col)), lds_tr4(tile + tile_off<D>(row + 8, col)));
-}
 __device__ __forceinline__ f16x8 to_f16x8(f32x4 a, f32x4 b, float s) {
     f16x8 r;
     r[0] = (_Float16)(a[0] * s); r[1] = (_Float16)(a[1] * s); r[2] = (_Float16)(a[2] * s); r[3] = (_Float16)(a[3] * s);
@@ -94,43 +87,141 @@ __device__ __forceinline__ f16x8 load_frag(const float* __restrict__ p, bool val
     return to_f16x8(v[0], v[1], s);
 }
 
+// Per-lane LDS element offsets into a swizzled [rows][D] fp16 tile.  The swizzle
+// only reads row bits 0..3, so one set serves every 32-row block and 16-row
+// sub-step (those add row*D constants the compiler folds into ds_read offsets).
+template <int D>
+struct FragOffsets {
+    int row[D / 16];    // A operand from rows: row lane&31, k-chunk 2t + lane>>5
+    int tr[D / 32][2];  // transposed operand (tr_operand), rows +0 and +8
+    __device__ __forceinline__ void init(int lane) {
+        const int r = lane & 31, h = lane >> 5, g = lane >> 4, i = lane & 15;
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) row[t] = tile_off<D>(r, 16 * t + 8 * h);
+        const int rt = 4 * (g >> 1) + (i >> 2), ct = 16 * (g & 1) + 4 * (i & 3);
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b) {
+            tr[b][0] = tile_off<D>(rt, 32 * b + ct);
+            tr[b][1] = tile_off<D>(rt + 8, 32 * b + ct);
+        }
+    }
+    // A operand, k over rows r0 .. r0+15 of the tile (r0 multiple of 16), columns 32b..32b+31
+    __device__ __forceinline__ f16x8 trop(const _Float16* tile, int r0, int b) const {
+        return cat4(lds_tr4(tile + tr[b][0] + r0 * D), lds_tr4(tile + tr[b][1] + r0 * D));
+    }
+    // A operand, rows r0 + (lane&31), k-chunk t
+    __device__ __forceinline__ f16x8 rowop(const _Float16* tile, int r0, int t) const {
+        return lds_row8(tile + row[t] + r0 * D);
+    }
+};
+
+// Register-staged tile loader: ROWS x D fp32 rows of a [S][D] tensor -> fp16
+// swizzled LDS, CPT chunks (8 floats) per thread.  Offsets are computed once;
+// full tiles take an unguarded path, the ragged last tile zero-fills rows >= S.
 template <int D, int ROWS, int NT>
 struct TileStager {
     static constexpr int CPR = D / 8;
     static constexpr int CHUNKS = ROWS * CPR;
     static constexpr int CPT = (CHUNKS + NT - 1) / NT;
+    static constexpr bool EXACT = CHUNKS % NT == 0;
     f32x4 r[CPT][2];
-    __device__ __forceinline__ void load(const float* __restrict__ src, int row0, int S, int tid) {
+    int goff[CPT], loff[CPT], grow[CPT];
+
+    __device__ __forceinline__ void init(int tid) {
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
             const int x = tid + c * NT;
             const int row = x / CPR, ch = x % CPR;
-            if ((CHUNKS % NT == 0 || x < CHUNKS) && row0 + row < S) {
-                const f32x4* p = reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * D + ch * 8);
-                r[c][0] = p[0];
-                r[c][1] = p[1];
-            } else {
-                r[c][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-                r[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            goff[c] = row * D + ch * 8;
+            loff[c] = row * D + ((ch ^ Swz<D>::f(row)) << 3);
+            grow[c] = (EXACT || x < CHUNKS) ? row : (1 << 30);
+        }
+    }
+    // src points at row 0 of the tile; nvalid = rows of the tile that exist
+    __device__ __forceinline__ void load(const float* __restrict__ src, int nvalid) {
+        if (nvalid >= ROWS) {
+#pragma unroll
+            for (int c = 0; c < CPT; ++c) {
+                if (EXACT || grow[c] < ROWS) {
+                    const f32x4* p = reinterpret_cast<const f32x4*>(src + goff[c]);
+                    r[c][0] = p[0];
+                    r[c][1] = p[1];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < CPT; ++c) {
+                if (grow[c] < nvalid) {
+                    const f32x4* p = reinterpret_cast<const f32x4*>(src + goff[c]);
+                    r[c][0] = p[0];
+                    r[c][1] = p[1];
+                } else {
+                    r[c][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    r[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
             }
         }
     }
-    __device__ __forceinline__ void store(_Float16* tile, int tid) const {
+    __device__ __forceinline__ void store(_Float16* tile, float scale) const {
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) {
-            const int x = tid + c * NT;
-            if (CHUNKS % NT == 0 || x < CHUNKS) {
-                const int row = x / CPR, ch = x % CPR;
-                *reinterpret_cast<f16x8*>(tile + row * D + ((ch ^ Swz<D>::f(row)) << 3)) =
-                    to_f16x8(r[c][0], r[c][1], 1.f);
-            }
-        }
+        for (int c = 0; c < CPT; ++c)
+            if (EXACT || grow[c] < ROWS) *reinterpret_cast<f16x8*>(tile + loff[c]) = to_f16x8(r[c][0], r[c][1], scale);
     }
 };
 
 // ---------------------------------------------------------------------------
 // dK, dV:  grid BH * ceil(S / (32*NW)), block 64*NW
 // ---------------------------------------------------------------------------
+template <int D>
+struct DkdvState {
+    f16x8 kf[D / 16], vf[D / 16];  // B operands: this lane's key row of K (scaled) and V
+    f32x16 dka[D / 32], dva[D / 32];
+};
+
+// One 64-query step: S = Q K^T and dP = dO V^T with the key on the lane (their
+// accumulators start at -LSE*log2e and -Delta), P = exp2(S), dS = P*(dP - Delta),
+// then dV^T += dO^T P and dK^T += Q^T dS with P / dS packed as B operands.
+template <int D>
+__device__ __forceinline__ void dkdv_step(DkdvState<D>& st, const _Float16* Qs, const _Float16* dOs,
+                                          const float* lse2, const float* del, const FragOffsets<D>& fo, int h) {
+    f16x8 pf[2][2], dsf[2][2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+        // accumulator rows: query qb*32 + (i&3) + 8*(i>>2) + 4h ; col: key (lane)
+        f32x16 sa, da;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2 + qb * 32 + 8 * g + 4 * h);
+            const f32x4 dv = *reinterpret_cast<const f32x4*>(del + qb * 32 + 8 * g + 4 * h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                sa[4 * g + e] = -lv[e];
+                da[4 * g + e] = -dv[e];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) {
+            sa = mfma(fo.rowop(Qs, qb * 32, t), st.kf[t], sa);
+            da = mfma(fo.rowop(dOs, qb * 32, t), st.vf[t], da);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float p = fast_exp2(sa[i]);
+            pf[qb][i >> 3][i & 7] = (_Float16)p;
+            dsf[qb][i >> 3][i & 7] = (_Float16)(p * da[i]);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                st.dva[b] = mfma(fo.trop(dOs, qb * 32 + 16 * s, b), pf[qb][s], st.dva[b]);
+                st.dka[b] = mfma(fo.trop(Qs, qb * 32 + 16 * s, b), dsf[qb][s], st.dka[b]);
+            }
+}
+
 template <int D, int NW>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
@@ -153,23 +244,27 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     const bool kvalid = key < S;
     const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
 
-    // K (pre-scaled by log2e/sqrt(D)) and V fragments: B operands, lane holds row `key`
-    f16x8 kf[D / 16], vf[D / 16];
+    DkdvState<D> st;
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
-        kf[t] = load_frag(K + base + (long)key * D + 16 * t + 8 * h, kvalid, kscale);
-        vf[t] = load_frag(V + base + (long)key * D + 16 * t + 8 * h, kvalid, 1.f);
+        st.kf[t] = load_frag(K + base + (long)key * D + 16 * t + 8 * h, kvalid, kscale);
+        st.vf[t] = load_frag(V + base + (long)key * D + 16 * t + 8 * h, kvalid, 1.f);
     }
-    f32x16 dka[D / 32], dva[D / 32];
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            dka[b][i] = 0.f;
-            dva[b][i] = 0.f;
+            st.dka[b][i] = 0.f;
+            st.dva[b][i] = 0.f;
         }
 
+    FragOffsets<D> fo;
+    fo.init(lane);
     TileStager<D, QT, NT> qs, dos;
+    qs.init(tid);
+    dos.init(tid);
+    const float* Qb = Q + base;
+    const float* dOb = dO + base;
     float rowv = 0.f;  // lse2 (threads [0,QT)) or delta (threads [QT,2QT)) of the staged step
     auto load_rows = [&](int q0) {
         if (tid < 2 * QT) {
@@ -181,75 +276,42 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     auto store_rows = [&](int buf) {
         if (tid < 2 * QT) rows[buf][tid / QT][tid & (QT - 1)] = rowv;
     };
+    auto load_step = [&](int it) {
+        qs.load(Qb + (long)it * QT * D, S - it * QT);
+        dos.load(dOb + (long)it * QT * D, S - it * QT);
+        load_rows(it * QT);
+    };
 
     const int nsteps = (S + QT - 1) / QT;
-    qs.load(Q + base, 0, S, tid);
-    dos.load(dO + base, 0, S, tid);
-    load_rows(0);
-    qs.store(smem, tid);
-    dos.store(smem + TILE, tid);
+    load_step(0);
+    qs.store(smem, 1.f);
+    dos.store(smem + TILE, 1.f);
     store_rows(0);
     __syncthreads();
 
-    for (int it = 0; it < nsteps; ++it) {
-        const int cur = it & 1;
-        const _Float16* Qs = smem + cur * 2 * TILE;
-        const _Float16* dOs = Qs + TILE;
-        const float* lse2 = rows[cur][0];
-        const float* del = rows[cur][1];
-        const bool more = it + 1 < nsteps;
-        if (more) {
-            qs.load(Q + base, (it + 1) * QT, S, tid);
-            dos.load(dO + base, (it + 1) * QT, S, tid);
-            load_rows((it + 1) * QT);
-        }
-
-        f16x8 pf[2][2], dsf[2][2];
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-            // accumulator rows: query qb*32 + (i&3) + 8*(i>>2) + 4h ; col: key (lane)
-            f32x16 sa, da;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2 + qb * 32 + 8 * g + 4 * h);
-                const f32x4 dv = *reinterpret_cast<const f32x4*>(del + qb * 32 + 8 * g + 4 * h);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    sa[4 * g + e] = -lv[e];
-                    da[4 * g + e] = -dv[e];
-                }
+    for (int it = 0; it < nsteps; it += 2) {
+        {
+            const bool more = it + 1 < nsteps;
+            if (more) load_step(it + 1);
+            dkdv_step<D>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h);
+            if (more) {
+                qs.store(smem + 2 * TILE, 1.f);
+                dos.store(smem + 3 * TILE, 1.f);
+                store_rows(1);
             }
-#pragma unroll
-            for (int t = 0; t < D / 16; ++t) {
-                const int off = tile_off<D>(qb * 32 + r, 16 * t + 8 * h);
-                sa = mfma(lds_row8(Qs + off), kf[t], sa);
-                da = mfma(lds_row8(dOs + off), vf[t], da);
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const float p = fast_exp2(sa[i]);
-                pf[qb][i >> 3][i & 7] = (_Float16)p;
-                dsf[qb][i >> 3][i & 7] = (_Float16)(p * da[i]);
-            }
+            __syncthreads();
         }
-        // dV^T += dO^T P ;  dK^T += Q^T dS   (k = query rows of this step)
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    dva[b] = mfma(tr_operand<D>(dOs, qb * 32 + 16 * s, 32 * b, lane), pf[qb][s], dva[b]);
-                    dka[b] = mfma(tr_operand<D>(Qs, qb * 32 + 16 * s, 32 * b, lane), dsf[qb][s], dka[b]);
-                }
-
-        if (more) {
-            _Float16* nxt = smem + (cur ^ 1) * 2 * TILE;
-            qs.store(nxt, tid);
-            dos.store(nxt + TILE, tid);
-            store_rows(cur ^ 1);
+        if (it + 1 < nsteps) {
+            const bool more = it + 2 < nsteps;
+            if (more) load_step(it + 2);
+            dkdv_step<D>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h);
+            if (more) {
+                qs.store(smem, 1.f);
+                dos.store(smem + TILE, 1.f);
+                store_rows(0);
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
 
     if (kvalid) {
@@ -260,9 +322,9 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
         for (int b = 0; b < D / 32; ++b)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                f32x4 a = {dka[b][4 * g] * dscale, dka[b][4 * g + 1] * dscale, dka[b][4 * g + 2] * dscale,
-                           dka[b][4 * g + 3] * dscale};
-                f32x4 c = {dva[b][4 * g], dva[b][4 * g + 1], dva[b][4 * g + 2], dva[b][4 * g + 3]};
+                f32x4 a = {st.dka[b][4 * g] * dscale, st.dka[b][4 * g + 1] * dscale, st.dka[b][4 * g + 2] * dscale,
+                           st.dka[b][4 * g + 3] * dscale};
+                f32x4 c = {st.dva[b][4 * g], st.dva[b][4 * g + 1], st.dva[b][4 * g + 2], st.dva[b][4 * g + 3]};
                 *reinterpret_cast<f32x4*>(dkrow + 32 * b + 8 * g + 4 * h) = a;
                 *reinterpret_cast<f32x4*>(dvrow + 32 * b + 8 * g + 4 * h) = c;
             }
@@ -272,6 +334,49 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
 // ---------------------------------------------------------------------------
 // dQ:  grid BH * ceil(S / (32*NW)), block 64*NW
 // ---------------------------------------------------------------------------
+template <int D>
+struct DqState {
+    f16x8 qf[D / 16], df[D / 16];  // B operands: this lane's query row of Q (scaled) and dO
+    f32x16 dqa[D / 32];
+    float lse2, del;
+};
+
+// One 64-key tile: S^T = K Q^T and dP^T = V dO^T with the query on the lane,
+// dS^T = P^T*(dP^T - Delta), dQ^T += K^T dS^T (K^T through ds_read_b64_tr_b16).
+template <int D>
+__device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, const _Float16* Vs,
+                                        const FragOffsets<D>& fo, int k0, int S, int h) {
+    f16x8 dsf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        // rows: key k0 + kb*32 + (i&3) + 8*(i>>2) + 4h ; col: query (lane)
+        f32x16 sa, da;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            sa[i] = -st.lse2;
+            da[i] = -st.del;
+        }
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) {
+            sa = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], sa);
+            da = mfma(fo.rowop(Vs, kb * 32, t), st.df[t], da);
+        }
+        if (k0 + 64 > S) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sa[i] = -__builtin_inff();
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dsf[kb][i >> 3][i & 7] = (_Float16)(fast_exp2(sa[i]) * da[i]);
+    }
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) st.dqa[b] = mfma(fo.trop(Ks, kb * 32 + 16 * s, b), dsf[kb][s], st.dqa[b]);
+}
+
 template <int D, int NW>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
@@ -291,76 +396,60 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     const bool qvalid = q < S;
     const float qscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
 
-    f16x8 qf[D / 16], df[D / 16];
+    DqState<D> st;
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
-        qf[t] = load_frag(Q + base + (long)q * D + 16 * t + 8 * h, qvalid, qscale);
-        df[t] = load_frag(dO + base + (long)q * D + 16 * t + 8 * h, qvalid, 1.f);
+        st.qf[t] = load_frag(Q + base + (long)q * D + 16 * t + 8 * h, qvalid, qscale);
+        st.df[t] = load_frag(dO + base + (long)q * D + 16 * t + 8 * h, qvalid, 1.f);
     }
-    const float lse2 = qvalid ? LSE[(long)bh * S + q] * FA2B_LOG2E : __builtin_inff();
-    const float del = qvalid ? Delta[(long)bh * S + q] : 0.f;
-
-    f32x16 dqa[D / 32];
+    st.lse2 = qvalid ? LSE[(long)bh * S + q] * FA2B_LOG2E : __builtin_inff();
+    st.del = qvalid ? Delta[(long)bh * S + q] : 0.f;
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dqa[b][i] = 0.f;
+        for (int i = 0; i < 16; ++i) st.dqa[b][i] = 0.f;
 
-    const int ntiles = (S + KT - 1) / KT;
+    FragOffsets<D> fo;
+    fo.init(lane);
     TileStager<D, KT, NT> ks, vs;
-    ks.load(K + base, 0, S, tid);
-    vs.load(V + base, 0, S, tid);
-    ks.store(smem, tid);
-    vs.store(smem + TILE, tid);
+    ks.init(tid);
+    vs.init(tid);
+    const float* Kb = K + base;
+    const float* Vb = V + base;
+    const int ntiles = (S + KT - 1) / KT;
+    ks.load(Kb, S);
+    vs.load(Vb, S);
+    ks.store(smem, 1.f);
+    vs.store(smem + TILE, 1.f);
     __syncthreads();
 
-    for (int j = 0; j < ntiles; ++j) {
-        const _Float16* Ks = smem + (j & 1) * 2 * TILE;
-        const _Float16* Vs = Ks + TILE;
-        const bool more = j + 1 < ntiles;
-        if (more) {
-            ks.load(K + base, (j + 1) * KT, S, tid);
-            vs.load(V + base, (j + 1) * KT, S, tid);
-        }
-        const int k0 = j * KT;
-        f16x8 dsf[2][2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            // rows: key k0 + kb*32 + (i&3) + 8*(i>>2) + 4h ; col: query (lane)
-            f32x16 sa, da;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                sa[i] = -lse2;
-                da[i] = -del;
+    for (int j = 0; j < ntiles; j += 2) {
+        {
+            const bool more = j + 1 < ntiles;
+            if (more) {
+                ks.load(Kb + (long)(j + 1) * KT * D, S - (j + 1) * KT);
+                vs.load(Vb + (long)(j + 1) * KT * D, S - (j + 1) * KT);
             }
-#pragma unroll
-            for (int t = 0; t < D / 16; ++t) {
-                const int off = tile_off<D>(kb * 32 + r, 16 * t + 8 * h);
-                sa = mfma(lds_row8(Ks + off), qf[t], sa);
-                da = mfma(lds_row8(Vs + off), df[t], da);
+            dq_tile<D>(st, smem, smem + TILE, fo, j * KT, S, h);
+            if (more) {
+                ks.store(smem + 2 * TILE, 1.f);
+                vs.store(smem + 3 * TILE, 1.f);
             }
-            const bool edge = k0 + KT > S;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                float p = fast_exp2(sa[i]);
-                if (edge && k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) p = 0.f;
-                dsf[kb][i >> 3][i & 7] = (_Float16)(p * da[i]);
+            __syncthreads();
+        }
+        if (j + 1 < ntiles) {
+            const bool more = j + 2 < ntiles;
+            if (more) {
+                ks.load(Kb + (long)(j + 2) * KT * D, S - (j + 2) * KT);
+                vs.load(Vb + (long)(j + 2) * KT * D, S - (j + 2) * KT);
             }
+            dq_tile<D>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
+            if (more) {
+                ks.store(smem, 1.f);
+                vs.store(smem + TILE, 1.f);
+            }
+            __syncthreads();
         }
-        // dQ^T += K^T dS^T  (k = key rows of this tile)
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int s = 0; s < 2; ++s)
-                    dqa[b] = mfma(tr_operand<D>(Ks, kb * 32 + 16 * s, 32 * b, lane), dsf[kb][s], dqa[b]);
-        if (more) {
-            _Float16* nxt = smem + ((j + 1) & 1) * 2 * TILE;
-            ks.store(nxt, tid);
-            vs.store(nxt + TILE, tid);
-        }
-        __syncthreads();
     }
 
     if (qvalid) {
@@ -370,8 +459,8 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
         for (int b = 0; b < D / 32; ++b)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                f32x4 a = {dqa[b][4 * g] * dscale, dqa[b][4 * g + 1] * dscale, dqa[b][4 * g + 2] * dscale,
-                           dqa[b][4 * g + 3] * dscale};
+                f32x4 a = {st.dqa[b][4 * g] * dscale, st.dqa[b][4 * g + 1] * dscale, st.dqa[b][4 * g + 2] * dscale,
+                           st.dqa[b][4 * g + 3] * dscale};
                 *reinterpret_cast<f32x4*>(row + 32 * b + 8 * g + 4 * h) = a;
             }
     }

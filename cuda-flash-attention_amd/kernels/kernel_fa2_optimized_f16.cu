@@ -81,18 +81,6 @@ __device__ __forceinline__ f16x8 cat4(i16x4 a, i16x4 b) {
     return __builtin_bit_cast(f16x8, c);
 }
 
-// A operand of a 32x32x16 MFMA whose k index runs over rows of a row-major tile
-// in the order an accumulator-as-B-operand imposes (guide: "accumulator tile as
-// the next MFMA's operand"): lane l gets column c0 + (l & 31) of rows
-// r0 + 4*(l>>5) + {0..3} and r0 + 8 + 4*(l>>5) + {0..3}.
-template <int D>
-__device__ __forceinline__ f16x8 tr_operand(const _Float16* tile, int r0, int c0, int lane) {
-    const int g = lane >> 4, i = lane & 15;
-    const int row = r0 + 4 * (g >> 1) + (i >> 2);
-    const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
-    return cat4(lds_tr4(tile + tile_off<D>(row, col)), lds_tr4(tile + tile_off<D>(row + 8, col)));
-}
-
 __device__ __forceinline__ f16x8 to_f16x8(f32x4 a, f32x4 b, float s) {
     f16x8 r;
     r[0] = (_Float16)(a[0] * s); r[1] = (_Float16)(a[1] * s); r[2] = (_Float16)(a[2] * s); r[3] = (_Float16)(a[3] * s);
@@ -106,47 +94,168 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
 }
 
-// Register-staged tile loader: ROWS x D fp32 rows [row0, row0+ROWS) of a [S][D]
-// tensor -> fp16 swizzled LDS.  Rows >= S load zeros.  CPT chunks (8 floats) per thread.
+// Per-lane LDS element offsets into a swizzled [rows][D] fp16 tile.  The swizzle
+// only reads row bits 0..3, so one set serves every 32-row block and 16-row
+// sub-step (those add row*D constants the compiler folds into ds_read offsets).
+template <int D>
+struct FragOffsets {
+    int row[D / 16];    // A operand from rows: row lane&31, k-chunk 2t + lane>>5
+    int tr[D / 32][2];  // transposed operand (tr_operand), rows +0 and +8
+    __device__ __forceinline__ void init(int lane) {
+        const int r = lane & 31, h = lane >> 5, g = lane >> 4, i = lane & 15;
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) row[t] = tile_off<D>(r, 16 * t + 8 * h);
+        const int rt = 4 * (g >> 1) + (i >> 2), ct = 16 * (g & 1) + 4 * (i & 3);
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b) {
+            tr[b][0] = tile_off<D>(rt, 32 * b + ct);
+            tr[b][1] = tile_off<D>(rt + 8, 32 * b + ct);
+        }
+    }
+    // A operand, k over rows r0 .. r0+15 of the tile (r0 multiple of 16), columns 32b..32b+31
+    __device__ __forceinline__ f16x8 trop(const _Float16* tile, int r0, int b) const {
+        return cat4(lds_tr4(tile + tr[b][0] + r0 * D), lds_tr4(tile + tr[b][1] + r0 * D));
+    }
+    // A operand, rows r0 + (lane&31), k-chunk t
+    __device__ __forceinline__ f16x8 rowop(const _Float16* tile, int r0, int t) const {
+        return lds_row8(tile + row[t] + r0 * D);
+    }
+};
+
+// Register-staged tile loader: ROWS x D fp32 rows of a [S][D] tensor -> fp16
+// swizzled LDS, CPT chunks (8 floats) per thread.  Offsets are computed once;
+// full tiles take an unguarded path, the ragged last tile zero-fills rows >= S.
 template <int D, int ROWS, int NT>
 struct TileStager {
     static constexpr int CPR = D / 8;
     static constexpr int CHUNKS = ROWS * CPR;
     static constexpr int CPT = (CHUNKS + NT - 1) / NT;
+    static constexpr bool EXACT = CHUNKS % NT == 0;
     f32x4 r[CPT][2];
+    int goff[CPT], loff[CPT], grow[CPT];
 
-    __device__ __forceinline__ void load(const float* __restrict__ src, int row0, int S, int tid) {
+    __device__ __forceinline__ void init(int tid) {
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
             const int x = tid + c * NT;
             const int row = x / CPR, ch = x % CPR;
-            if ((CHUNKS % NT == 0 || x < CHUNKS) && row0 + row < S) {
-                const f32x4* p = reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * D + ch * 8);
-                r[c][0] = p[0];
-                r[c][1] = p[1];
-            } else {
-                r[c][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-                r[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            goff[c] = row * D + ch * 8;
+            loff[c] = row * D + ((ch ^ Swz<D>::f(row)) << 3);
+            grow[c] = (EXACT || x < CHUNKS) ? row : (1 << 30);
+        }
+    }
+    // src points at row 0 of the tile; nvalid = rows of the tile that exist
+    __device__ __forceinline__ void load(const float* __restrict__ src, int nvalid) {
+        if (nvalid >= ROWS) {
+#pragma unroll
+            for (int c = 0; c < CPT; ++c) {
+                if (EXACT || grow[c] < ROWS) {
+                    const f32x4* p = reinterpret_cast<const f32x4*>(src + goff[c]);
+                    r[c][0] = p[0];
+                    r[c][1] = p[1];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < CPT; ++c) {
+                if (grow[c] < nvalid) {
+                    const f32x4* p = reinterpret_cast<const f32x4*>(src + goff[c]);
+                    r[c][0] = p[0];
+                    r[c][1] = p[1];
+                } else {
+                    r[c][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    r[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
             }
         }
     }
-    __device__ __forceinline__ void store(_Float16* tile, int tid, float scale) const {
+    __device__ __forceinline__ void store(_Float16* tile, float scale) const {
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) {
-            const int x = tid + c * NT;
-            if (CHUNKS % NT == 0 || x < CHUNKS) {
-                const int row = x / CPR, ch = x % CPR;
-                *reinterpret_cast<f16x8*>(tile + row * D + ((ch ^ Swz<D>::f(row)) << 3)) =
-                    to_f16x8(r[c][0], r[c][1], scale);
-            }
-        }
+        for (int c = 0; c < CPT; ++c)
+            if (EXACT || grow[c] < ROWS) *reinterpret_cast<f16x8*>(tile + loff[c]) = to_f16x8(r[c][0], r[c][1], scale);
     }
 };
+
+__device__ __forceinline__ float xor32_max(float x) {
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
 
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-// Grid: BH * ceil(S / (32*NW)) workgroups of 64*NW threads.
+// Online-softmax state of one wave: 32 query rows (one per lane pair), O^T
+// accumulator (d on the rows), running max m (log2 domain) and per-half sum l.
+template <int D>
+struct FwdState {
+    f16x8 qf[D / 16];
+    f32x16 oacc[D / 32];
+    float m, l;
+};
+
+// Lazy rescale (guide T13): the running max moves only when a tile's max
+// exceeds it by more than RESCALE_THR (log2 units), so p <= 2^8 in fp16/fp32.
+#define FA2_RESCALE_THR 8.0f
+
+// One 64-key tile: S^T = K Q^T (keys on registers, query on the lane), online
+// softmax, O^T += V^T P^T with the packed S^T accumulator as B operand.
+template <int D>
+__device__ __forceinline__ void fwd_tile(FwdState<D>& st, const _Float16* Ks, const _Float16* Vs,
+                                         const FragOffsets<D>& fo, int k0, int S, int h) {
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) sacc[kb] = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], sacc[kb]);
+    }
+    if (k0 + 64 > S) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[kb][i] = -__builtin_inff();
+    }
+    float mx = fmaxf(sacc[0][0], sacc[0][1]);
+#pragma unroll
+    for (int i = 2; i < 16; ++i) mx = fmaxf(mx, sacc[0][i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[1][i]);
+    mx = xor32_max(mx);
+    const bool grow = mx > st.m + FA2_RESCALE_THR;
+    if (__any(grow)) {
+        const float mnew = grow ? mx : st.m;
+        const float alpha = fast_exp2(st.m - mnew);
+        st.m = mnew;
+        st.l *= alpha;
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) st.oacc[b][i] *= alpha;
+    }
+    f16x8 pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float p = fast_exp2(sacc[kb][i] - st.m);
+            st.l += p;
+            pf[kb][i >> 3][i & 7] = (_Float16)p;
+        }
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) st.oacc[b] = mfma(fo.trop(Vs, kb * 32 + 16 * s, b), pf[kb][s], st.oacc[b]);
+}
+
+// Grid: BH * ceil(S / (32*NW)) workgroups of 64*NW threads (NW waves x 32 queries).
 template <int D, int NW>
 __global__ void __launch_bounds__(64 * NW)
 fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
@@ -154,7 +263,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     constexpr int KT = 64;  // keys per tile
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];  // [buf][K | V]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int nqb = (S + 32 * NW - 1) / (32 * NW);
@@ -164,104 +273,69 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     const int q = qb * 32 * NW + wave * 32 + r;
     const float qscale = FA2_LOG2E / __builtin_sqrtf((float)D);
 
+    FwdState<D> st;
     // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16t + 8h + 0..7]
-    f16x8 qf[D / 16];
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
         if (q < S) {
             const f32x4* p = reinterpret_cast<const f32x4*>(Q + base + (long)q * D + 16 * t + 8 * h);
-            qf[t] = to_f16x8(p[0], p[1], qscale);
+            st.qf[t] = to_f16x8(p[0], p[1], qscale);
         } else {
-            qf[t] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            st.qf[t] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
     }
-
-    f32x16 oacc[D / 32];
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) oacc[b][i] = 0.f;
-    float m = -__builtin_inff(), l = 0.f;
+        for (int i = 0; i < 16; ++i) st.oacc[b][i] = 0.f;
+    st.m = -__builtin_inff();
+    st.l = 0.f;
 
-    const int ntiles = (S + KT - 1) / KT;
+    FragOffsets<D> fo;
+    fo.init(lane);
     TileStager<D, KT, NT> ks, vs;
-    ks.load(K + base, 0, S, tid);
-    vs.load(V + base, 0, S, tid);
-    ks.store(smem, tid, 1.f);
-    vs.store(smem + TILE, tid, 1.f);
+    ks.init(tid);
+    vs.init(tid);
+    const float* Kb = K + base;
+    const float* Vb = V + base;
+    const int ntiles = (S + KT - 1) / KT;
+    ks.load(Kb, S);
+    vs.load(Vb, S);
+    ks.store(smem, 1.f);
+    vs.store(smem + TILE, 1.f);
     __syncthreads();
 
-    for (int j = 0; j < ntiles; ++j) {
-        const _Float16* Ks = smem + (j & 1) * 2 * TILE;
-        const _Float16* Vs = Ks + TILE;
-        const bool more = j + 1 < ntiles;
-        if (more) {
-            ks.load(K + base, (j + 1) * KT, S, tid);
-            vs.load(V + base, (j + 1) * KT, S, tid);
-        }
-
-        // S^T (64 keys x 32 queries) as two 32x32 blocks
-        f32x16 sacc[2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
-#pragma unroll
-            for (int t = 0; t < D / 16; ++t)
-                sacc[kb] = mfma(lds_row8(Ks + tile_off<D>(kb * 32 + r, 16 * t + 8 * h)), qf[t], sacc[kb]);
-        }
-        const int k0 = j * KT;
-        if (k0 + KT > S) {
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[kb][i] = -__builtin_inff();
-        }
-        // online softmax (row = this lane's query; the two half-waves hold 32 keys each)
-        float mx = sacc[0][0];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kb][i]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const float mnew = fmaxf(m, mx);
-        if (__any(mnew > m)) {
-            const float alpha = fast_exp2(m - mnew);
-            l *= alpha;
-#pragma unroll
-            for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) oacc[b][i] *= alpha;
-        }
-        m = mnew;
-        f16x8 pf[2][2];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const float p = fast_exp2(sacc[kb][i] - m);
-                l += p;
-                pf[kb][i >> 3][i & 7] = (_Float16)p;
+    // two tiles per trip so every LDS buffer offset is a compile-time immediate
+    for (int j = 0; j < ntiles; j += 2) {
+        {
+            const bool more = j + 1 < ntiles;
+            if (more) {
+                ks.load(Kb + (long)(j + 1) * KT * D, S - (j + 1) * KT);
+                vs.load(Vb + (long)(j + 1) * KT * D, S - (j + 1) * KT);
             }
-        // O^T += V^T P^T
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int s = 0; s < 2; ++s)
-                    oacc[b] = mfma(tr_operand<D>(Vs, kb * 32 + 16 * s, 32 * b, lane), pf[kb][s], oacc[b]);
-
-        if (more) {
-            _Float16* nxt = smem + ((j + 1) & 1) * 2 * TILE;
-            ks.store(nxt, tid, 1.f);
-            vs.store(nxt + TILE, tid, 1.f);
+            fwd_tile<D>(st, smem, smem + TILE, fo, j * KT, S, h);
+            if (more) {
+                ks.store(smem + 2 * TILE, 1.f);
+                vs.store(smem + 3 * TILE, 1.f);
+            }
+            __syncthreads();
         }
-        __syncthreads();
+        if (j + 1 < ntiles) {
+            const bool more = j + 2 < ntiles;
+            if (more) {
+                ks.load(Kb + (long)(j + 2) * KT * D, S - (j + 2) * KT);
+                vs.load(Vb + (long)(j + 2) * KT * D, S - (j + 2) * KT);
+            }
+            fwd_tile<D>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
+            if (more) {
+                ks.store(smem, 1.f);
+                vs.store(smem + TILE, 1.f);
+            }
+            __syncthreads();
+        }
     }
 
-    const float lt = l + __shfl_xor(l, 32);
+    const float lt = xor32_sum(st.l);
     const float inv = 1.f / lt;
     if (q < S) {
         float* orow = O + base + (long)q * D;
@@ -269,11 +343,11 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         for (int b = 0; b < D / 32; ++b)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                f32x4 v = {oacc[b][4 * g] * inv, oacc[b][4 * g + 1] * inv, oacc[b][4 * g + 2] * inv,
-                           oacc[b][4 * g + 3] * inv};
+                f32x4 v = {st.oacc[b][4 * g] * inv, st.oacc[b][4 * g + 1] * inv, st.oacc[b][4 * g + 2] * inv,
+                           st.oacc[b][4 * g + 3] * inv};
                 *reinterpret_cast<f32x4*>(orow + 32 * b + 8 * g + 4 * h) = v;
             }
-        if (h == 0) LSE[(long)bh * S + q] = m * FA2_LN2 + __logf(lt);
+        if (h == 0) LSE[(long)bh * S + q] = st.m * FA2_LN2 + __logf(lt);
     }
 }
 

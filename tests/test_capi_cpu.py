@@ -96,3 +96,16 @@ def test_cupy_face_compiles_under_hiprtc(fname, symbols):
     exported = rawmodule.exported_kernels(co)
     for s in symbols:
         assert s in exported
+
+
+@pytest.mark.parametrize("D", [32, 64, 128])
+def test_cupy_face_lds_budget(D):
+    """static LDS + the harness's dynamic LDS (test_flash_attention2.py:278-281, 522-527)
+    must fit the 160 KiB a workgroup may own, for every supported head_dim."""
+    fwd = rawmodule.static_lds_bytes(rawmodule.compile_source(rawmodule.load_kernel_source("kernel_fa2_optimized.cu")))
+    bwd = rawmodule.static_lds_bytes(rawmodule.compile_source(rawmodule.load_kernel_source("f-attn2-backward.cu")))
+    dyn_fwd = (32 * D * 2 + 32 * D + 32 * 32 + 32 * 3) * 4
+    dyn_bwd = (32 * D + 32 * D * 4 + 32 + 32 * 32) * 4
+    assert fwd["flash_attention2_forward_kernel_wrapper"] + dyn_fwd <= rawmodule.MAX_LDS_BYTES
+    assert bwd["flash_attention2_backward_kernel_wrapper"] + dyn_bwd <= rawmodule.MAX_LDS_BYTES
+    assert bwd["D_computation_reduction_kernel_wrapper"] + 64 * 4 <= rawmodule.MAX_LDS_BYTES
