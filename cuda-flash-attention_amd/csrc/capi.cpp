@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <thread>
@@ -55,6 +56,14 @@ struct DevBuf {
 };
 
 }  // namespace
+
+namespace fa2 {
+int tune_knob(const char* name, int dflt) {
+    std::string key = std::string("FA2_TUNE_") + name;
+    const char* v = getenv(key.c_str());
+    return v ? atoi(v) : dflt;
+}
+}  // namespace fa2
 
 extern "C" {
 

@@ -115,9 +115,24 @@ struct FragOffsets {
     }
 };
 
-// Register-staged tile loader: ROWS x D fp32 rows of a [S][D] tensor -> fp16
-// swizzled LDS, CPT chunks (8 floats) per thread.  Offsets are computed once;
-// full tiles take an unguarded path, the ragged last tile zero-fills rows >= S.
+// Buffer descriptor over one head's [S][D] fp32 rows: the hardware range check
+// returns zeros for rows >= S, so ragged tiles need no guards.  Built from
+// wave-uniform values only (readfirstlane), so no waterfall loops (guide T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const float* base, int S, int D) {
+    const unsigned long long a = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane(S * D * 4);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, bytes,
+                                             0x00020000);
+}
+__device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+// Register-staged tile loader: ROWS x D fp32 rows of one head's [S][D] tensor ->
+// fp16 swizzled LDS, CPT chunks (8 floats) per thread, byte offsets computed once;
+// buffer loads take the tile origin as a scalar offset (no per-load VALU).
 template <int D, int ROWS, int NT>
 struct TileStager {
     static constexpr int CPR = D / 8;
@@ -125,47 +140,33 @@ struct TileStager {
     static constexpr int CPT = (CHUNKS + NT - 1) / NT;
     static constexpr bool EXACT = CHUNKS % NT == 0;
     f32x4 r[CPT][2];
-    int goff[CPT], loff[CPT], grow[CPT];
+    int voff[CPT], loff[CPT];
+    __amdgpu_buffer_rsrc_t rs;
 
-    __device__ __forceinline__ void init(int tid) {
+    __device__ __forceinline__ void init(const float* head_base, int S, int tid) {
+        rs = head_rsrc(head_base, S, D);
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
             const int x = tid + c * NT;
             const int row = x / CPR, ch = x % CPR;
-            goff[c] = row * D + ch * 8;
+            voff[c] = (EXACT || x < CHUNKS) ? (row * D + ch * 8) * 4 : 0x7ffffff0;  // inactive: out of range
             loff[c] = row * D + ((ch ^ Swz<D>::f(row)) << 3);
-            grow[c] = (EXACT || x < CHUNKS) ? row : (1 << 30);
         }
     }
-    // src points at row 0 of the tile; nvalid = rows of the tile that exist
-    __device__ __forceinline__ void load(const float* __restrict__ src, int nvalid) {
-        if (nvalid >= ROWS) {
+    // rows [row0, row0 + ROWS); rows >= S read as zeros
+    __device__ __forceinline__ void load(int row0) {
+        const int soff = row0 * D * 4;
 #pragma unroll
-            for (int c = 0; c < CPT; ++c) {
-                if (EXACT || grow[c] < ROWS) {
-                    const f32x4* p = reinterpret_cast<const f32x4*>(src + goff[c]);
-                    r[c][0] = p[0];
-                    r[c][1] = p[1];
-                }
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < CPT; ++c) {
-                if (grow[c] < nvalid) {
-                    const f32x4* p = reinterpret_cast<const f32x4*>(src + goff[c]);
-                    r[c][0] = p[0];
-                    r[c][1] = p[1];
-                } else {
-                    r[c][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    r[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-                }
-            }
+        for (int c = 0; c < CPT; ++c) {
+            r[c][0] = buf_load4(rs, voff[c], soff);
+            r[c][1] = buf_load4(rs, voff[c] + 16, soff);
         }
     }
-    __device__ __forceinline__ void store(_Float16* tile, float scale) const {
+    __device__ __forceinline__ void store(_Float16* tile, float scale, int tid) const {
 #pragma unroll
         for (int c = 0; c < CPT; ++c)
-            if (EXACT || grow[c] < ROWS) *reinterpret_cast<f16x8*>(tile + loff[c]) = to_f16x8(r[c][0], r[c][1], scale);
+            if (EXACT || tid + c * NT < CHUNKS)
+                *reinterpret_cast<f16x8*>(tile + loff[c]) = to_f16x8(r[c][0], r[c][1], scale);
     }
 };
 
@@ -183,7 +184,7 @@ struct DkdvState {
 // then dV^T += dO^T P and dK^T += Q^T dS with P / dS packed as B operands.
 template <int D>
 __device__ __forceinline__ void dkdv_step(DkdvState<D>& st, const _Float16* Qs, const _Float16* dOs,
-                                          const float* lse2, const float* del, const FragOffsets<D>& fo, int h) {
+                                          const float* nlse2, const float* ndel, const FragOffsets<D>& fo, int h) {
     f16x8 pf[2][2], dsf[2][2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
@@ -191,12 +192,12 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D>& st, const _Float16* Qs, 
         f32x16 sa, da;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            const f32x4 lv = *reinterpret_cast<const f32x4*>(lse2 + qb * 32 + 8 * g + 4 * h);
-            const f32x4 dv = *reinterpret_cast<const f32x4*>(del + qb * 32 + 8 * g + 4 * h);
+            const f32x4 lv = *reinterpret_cast<const f32x4*>(nlse2 + qb * 32 + 8 * g + 4 * h);
+            const f32x4 dv = *reinterpret_cast<const f32x4*>(ndel + qb * 32 + 8 * g + 4 * h);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                sa[4 * g + e] = -lv[e];
-                da[4 * g + e] = -dv[e];
+                sa[4 * g + e] = lv[e];
+                da[4 * g + e] = dv[e];
             }
         }
 #pragma unroll
@@ -230,7 +231,7 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     constexpr int QT = 64;  // query rows per step
     constexpr int NT = 64 * NW;
     constexpr int TILE = QT * D;
-    // [buf][Q | dO] fp16 tiles, then [buf][lse2 | delta] fp32 rows
+    // [buf][Q | dO] fp16 tiles, then [buf][-lse2 | -delta] fp32 rows
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
     __shared__ __attribute__((aligned(16))) float rows[2][2][QT];
 
@@ -261,31 +262,30 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     FragOffsets<D> fo;
     fo.init(lane);
     TileStager<D, QT, NT> qs, dos;
-    qs.init(tid);
-    dos.init(tid);
-    const float* Qb = Q + base;
-    const float* dOb = dO + base;
-    float rowv = 0.f;  // lse2 (threads [0,QT)) or delta (threads [QT,2QT)) of the staged step
+    qs.init(Q + base, S, tid);
+    dos.init(dO + base, S, tid);
+    float rowv = 0.f;  // -lse2 (threads [0,QT)) or -delta (threads [QT,2QT)) of the staged step
     auto load_rows = [&](int q0) {
         if (tid < 2 * QT) {
             const int qi = q0 + (tid & (QT - 1));
-            if (tid < QT) rowv = qi < S ? LSE[rbase + qi] * FA2B_LOG2E : __builtin_inff();
-            else rowv = qi < S ? Delta[rbase + qi] : 0.f;
+            // stored negated: they are the initial accumulators of S and dP
+            if (tid < QT) rowv = qi < S ? -LSE[rbase + qi] * FA2B_LOG2E : -__builtin_inff();
+            else rowv = qi < S ? -Delta[rbase + qi] : 0.f;
         }
     };
     auto store_rows = [&](int buf) {
         if (tid < 2 * QT) rows[buf][tid / QT][tid & (QT - 1)] = rowv;
     };
     auto load_step = [&](int it) {
-        qs.load(Qb + (long)it * QT * D, S - it * QT);
-        dos.load(dOb + (long)it * QT * D, S - it * QT);
+        qs.load(it * QT);
+        dos.load(it * QT);
         load_rows(it * QT);
     };
 
     const int nsteps = (S + QT - 1) / QT;
     load_step(0);
-    qs.store(smem, 1.f);
-    dos.store(smem + TILE, 1.f);
+    qs.store(smem, 1.f, tid);
+    dos.store(smem + TILE, 1.f, tid);
     store_rows(0);
     __syncthreads();
 
@@ -295,8 +295,8 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
             if (more) load_step(it + 1);
             dkdv_step<D>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h);
             if (more) {
-                qs.store(smem + 2 * TILE, 1.f);
-                dos.store(smem + 3 * TILE, 1.f);
+                qs.store(smem + 2 * TILE, 1.f, tid);
+                dos.store(smem + 3 * TILE, 1.f, tid);
                 store_rows(1);
             }
             __syncthreads();
@@ -306,8 +306,8 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
             if (more) load_step(it + 2);
             dkdv_step<D>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h);
             if (more) {
-                qs.store(smem, 1.f);
-                dos.store(smem + TILE, 1.f);
+                qs.store(smem, 1.f, tid);
+                dos.store(smem + TILE, 1.f, tid);
                 store_rows(0);
             }
             __syncthreads();
@@ -338,30 +338,25 @@ template <int D>
 struct DqState {
     f16x8 qf[D / 16], df[D / 16];  // B operands: this lane's query row of Q (scaled) and dO
     f32x16 dqa[D / 32];
-    float lse2, del;
+    f32x16 nlse2, ndel;            // loop-invariant initial accumulators: -lse2, -delta (per lane)
 };
 
 // One 64-key tile: S^T = K Q^T and dP^T = V dO^T with the query on the lane,
 // dS^T = P^T*(dP^T - Delta), dQ^T += K^T dS^T (K^T through ds_read_b64_tr_b16).
-template <int D>
+template <int D, bool MASK>
 __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, const _Float16* Vs,
                                         const FragOffsets<D>& fo, int k0, int S, int h) {
     f16x8 dsf[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
         // rows: key k0 + kb*32 + (i&3) + 8*(i>>2) + 4h ; col: query (lane)
-        f32x16 sa, da;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            sa[i] = -st.lse2;
-            da[i] = -st.del;
-        }
+        f32x16 sa = st.nlse2, da = st.ndel;
 #pragma unroll
         for (int t = 0; t < D / 16; ++t) {
             sa = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], sa);
             da = mfma(fo.rowop(Vs, kb * 32, t), st.df[t], da);
         }
-        if (k0 + 64 > S) {
+        if (MASK) {  // ragged last tile only
 #pragma unroll
             for (int i = 0; i < 16; ++i)
                 if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sa[i] = -__builtin_inff();
@@ -402,8 +397,15 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
         st.qf[t] = load_frag(Q + base + (long)q * D + 16 * t + 8 * h, qvalid, qscale);
         st.df[t] = load_frag(dO + base + (long)q * D + 16 * t + 8 * h, qvalid, 1.f);
     }
-    st.lse2 = qvalid ? LSE[(long)bh * S + q] * FA2B_LOG2E : __builtin_inff();
-    st.del = qvalid ? Delta[(long)bh * S + q] : 0.f;
+    {
+        const float nl = qvalid ? -LSE[(long)bh * S + q] * FA2B_LOG2E : -__builtin_inff();
+        const float nd = qvalid ? -Delta[(long)bh * S + q] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            st.nlse2[i] = nl;
+            st.ndel[i] = nd;
+        }
+    }
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
@@ -412,41 +414,42 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     FragOffsets<D> fo;
     fo.init(lane);
     TileStager<D, KT, NT> ks, vs;
-    ks.init(tid);
-    vs.init(tid);
-    const float* Kb = K + base;
-    const float* Vb = V + base;
+    ks.init(K + base, S, tid);
+    vs.init(V + base, S, tid);
     const int ntiles = (S + KT - 1) / KT;
-    ks.load(Kb, S);
-    vs.load(Vb, S);
-    ks.store(smem, 1.f);
-    vs.store(smem + TILE, 1.f);
+    const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
+    ks.load(0);
+    vs.load(0);
+    ks.store(smem, 1.f, tid);
+    vs.store(smem + TILE, 1.f, tid);
     __syncthreads();
 
     for (int j = 0; j < ntiles; j += 2) {
         {
             const bool more = j + 1 < ntiles;
             if (more) {
-                ks.load(Kb + (long)(j + 1) * KT * D, S - (j + 1) * KT);
-                vs.load(Vb + (long)(j + 1) * KT * D, S - (j + 1) * KT);
+                ks.load((j + 1) * KT);
+                vs.load((j + 1) * KT);
             }
-            dq_tile<D>(st, smem, smem + TILE, fo, j * KT, S, h);
+            if (j == last_ragged) dq_tile<D, true>(st, smem, smem + TILE, fo, j * KT, S, h);
+            else dq_tile<D, false>(st, smem, smem + TILE, fo, j * KT, S, h);
             if (more) {
-                ks.store(smem + 2 * TILE, 1.f);
-                vs.store(smem + 3 * TILE, 1.f);
+                ks.store(smem + 2 * TILE, 1.f, tid);
+                vs.store(smem + 3 * TILE, 1.f, tid);
             }
             __syncthreads();
         }
         if (j + 1 < ntiles) {
             const bool more = j + 2 < ntiles;
             if (more) {
-                ks.load(Kb + (long)(j + 2) * KT * D, S - (j + 2) * KT);
-                vs.load(Vb + (long)(j + 2) * KT * D, S - (j + 2) * KT);
+                ks.load((j + 2) * KT);
+                vs.load((j + 2) * KT);
             }
-            dq_tile<D>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
+            if (j + 1 == last_ragged) dq_tile<D, true>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
+            else dq_tile<D, false>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
             if (more) {
-                ks.store(smem, 1.f);
-                vs.store(smem + TILE, 1.f);
+                ks.store(smem, 1.f, tid);
+                vs.store(smem + TILE, 1.f, tid);
             }
             __syncthreads();
         }
@@ -474,13 +477,9 @@ namespace fa2 {
 namespace {
 // waves per workgroup: 8 x 32 keys for D <= 64 (2 waves/SIMD fit in 256 VGPRs);
 // D = 128 needs more than 256 registers per lane, so 4 waves (1 per SIMD).
-template <int D> struct DkdvWaves { static constexpr int value = D <= 64 ? 8 : 4; };
-constexpr int kDqWaves = 4;
-
-template <int D>
-hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
-                         const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-    constexpr int NW = DkdvWaves<D>::value;
+template <int D, int NW>
+hipError_t dkdv_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                       const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
     const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream,
@@ -488,13 +487,27 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     return hipGetLastError();
 }
 template <int D>
+hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                         const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
+    const int nw = tune_knob("DKDV_WAVES", D <= 64 ? 8 : 4);
+    if (nw == 8 && D <= 64) return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+    return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+}
+template <int D, int NW>
+hipError_t dq_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                     const float* delta, float* dq, int bh, int S, hipStream_t stream) {
+    const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q,
+                       k, v, dout, lse, delta, dq, S);
+    return hipGetLastError();
+}
+template <int D>
 hipError_t dq_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                        const float* delta, float* dq, int bh, int S, hipStream_t stream) {
-    const long grid = (long)bh * ((S + 32 * kDqWaves - 1) / (32 * kDqWaves));
-    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, kDqWaves>), dim3((unsigned)grid), dim3(64 * kDqWaves), 0,
-                       stream, q, k, v, dout, lse, delta, dq, S);
-    return hipGetLastError();
+    const int nw = tune_knob("DQ_WAVES", 8);
+    if (nw == 8) return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, stream);
+    return dq_launch<D, 4>(q, k, v, dout, lse, delta, dq, bh, S, stream);
 }
 }  // namespace
 

@@ -65,8 +65,8 @@ hipError_t launch_delta(int D, const float* dout, const float* o, float* delta, 
 hipError_t launch_backward_f16(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream);
-// exact-fp32 backward; dq must be zeroed by the caller (it accumulates with
-// global fp32 atomics, as f-attn2-backward.cu:298 does).
+// exact-fp32 backward; dq is zeroed here (hipMemsetAsync on `stream`) and then
+// accumulated with global fp32 atomics, as f-attn2-backward.cu:298 does.
 hipError_t launch_backward_f32(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream);
@@ -79,5 +79,10 @@ hipError_t launch_bwd_dq_f16(int D, const float* q, const float* k, const float*
                              const float* lse, const float* delta, float* dq, int bh, int S, hipStream_t stream);
 
 inline bool supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
+
+// Launch-geometry knob read from the environment at each launch (FA2_TUNE_<NAME>=value),
+// used to A/B kernel variants in one process (tools/kbench.py); `dflt` is the
+// measured best and what ships.
+int tune_knob(const char* name, int dflt);
 
 }  // namespace fa2

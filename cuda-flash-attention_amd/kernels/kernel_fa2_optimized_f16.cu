@@ -122,9 +122,24 @@ struct FragOffsets {
     }
 };
 
-// Register-staged tile loader: ROWS x D fp32 rows of a [S][D] tensor -> fp16
-// swizzled LDS, CPT chunks (8 floats) per thread.  Offsets are computed once;
-// full tiles take an unguarded path, the ragged last tile zero-fills rows >= S.
+// Buffer descriptor over one head's [S][D] fp32 rows: the hardware range check
+// returns zeros for rows >= S, so ragged tiles need no guards.  Built from
+// wave-uniform values only (readfirstlane), so no waterfall loops (guide T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const float* base, int S, int D) {
+    const unsigned long long a = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane(S * D * 4);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, bytes,
+                                             0x00020000);
+}
+__device__ __forceinline__ f32x4 buf_load4(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+// Register-staged tile loader: ROWS x D fp32 rows of one head's [S][D] tensor ->
+// fp16 swizzled LDS, CPT chunks (8 floats) per thread, byte offsets computed once;
+// buffer loads take the tile origin as a scalar offset (no per-load VALU).
 template <int D, int ROWS, int NT>
 struct TileStager {
     static constexpr int CPR = D / 8;
@@ -132,47 +147,33 @@ struct TileStager {
     static constexpr int CPT = (CHUNKS + NT - 1) / NT;
     static constexpr bool EXACT = CHUNKS % NT == 0;
     f32x4 r[CPT][2];
-    int goff[CPT], loff[CPT], grow[CPT];
+    int voff[CPT], loff[CPT];
+    __amdgpu_buffer_rsrc_t rs;
 
-    __device__ __forceinline__ void init(int tid) {
+    __device__ __forceinline__ void init(const float* head_base, int S, int tid) {
+        rs = head_rsrc(head_base, S, D);
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
             const int x = tid + c * NT;
             const int row = x / CPR, ch = x % CPR;
-            goff[c] = row * D + ch * 8;
+            voff[c] = (EXACT || x < CHUNKS) ? (row * D + ch * 8) * 4 : 0x7ffffff0;  // inactive: out of range
             loff[c] = row * D + ((ch ^ Swz<D>::f(row)) << 3);
-            grow[c] = (EXACT || x < CHUNKS) ? row : (1 << 30);
         }
     }
-    // src points at row 0 of the tile; nvalid = rows of the tile that exist
-    __device__ __forceinline__ void load(const float* __restrict__ src, int nvalid) {
-        if (nvalid >= ROWS) {
+    // rows [row0, row0 + ROWS); rows >= S read as zeros
+    __device__ __forceinline__ void load(int row0) {
+        const int soff = row0 * D * 4;
 #pragma unroll
-            for (int c = 0; c < CPT; ++c) {
-                if (EXACT || grow[c] < ROWS) {
-                    const f32x4* p = reinterpret_cast<const f32x4*>(src + goff[c]);
-                    r[c][0] = p[0];
-                    r[c][1] = p[1];
-                }
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < CPT; ++c) {
-                if (grow[c] < nvalid) {
-                    const f32x4* p = reinterpret_cast<const f32x4*>(src + goff[c]);
-                    r[c][0] = p[0];
-                    r[c][1] = p[1];
-                } else {
-                    r[c][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    r[c][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-                }
-            }
+        for (int c = 0; c < CPT; ++c) {
+            r[c][0] = buf_load4(rs, voff[c], soff);
+            r[c][1] = buf_load4(rs, voff[c] + 16, soff);
         }
     }
-    __device__ __forceinline__ void store(_Float16* tile, float scale) const {
+    __device__ __forceinline__ void store(_Float16* tile, float scale, int tid) const {
 #pragma unroll
         for (int c = 0; c < CPT; ++c)
-            if (EXACT || grow[c] < ROWS) *reinterpret_cast<f16x8*>(tile + loff[c]) = to_f16x8(r[c][0], r[c][1], scale);
+            if (EXACT || tid + c * NT < CHUNKS)
+                *reinterpret_cast<f16x8*>(tile + loff[c]) = to_f16x8(r[c][0], r[c][1], scale);
     }
 };
 
@@ -203,7 +204,7 @@ struct FwdState {
 
 // One 64-key tile: S^T = K Q^T (keys on registers, query on the lane), online
 // softmax, O^T += V^T P^T with the packed S^T accumulator as B operand.
-template <int D>
+template <int D, bool MASK>
 __device__ __forceinline__ void fwd_tile(FwdState<D>& st, const _Float16* Ks, const _Float16* Vs,
                                          const FragOffsets<D>& fo, int k0, int S, int h) {
     f32x16 sacc[2];
@@ -214,7 +215,7 @@ __device__ __forceinline__ void fwd_tile(FwdState<D>& st, const _Float16* Ks, co
 #pragma unroll
         for (int t = 0; t < D / 16; ++t) sacc[kb] = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], sacc[kb]);
     }
-    if (k0 + 64 > S) {
+    if (MASK) {  // ragged last tile only
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -294,15 +295,14 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     FragOffsets<D> fo;
     fo.init(lane);
     TileStager<D, KT, NT> ks, vs;
-    ks.init(tid);
-    vs.init(tid);
-    const float* Kb = K + base;
-    const float* Vb = V + base;
+    ks.init(K + base, S, tid);
+    vs.init(V + base, S, tid);
     const int ntiles = (S + KT - 1) / KT;
-    ks.load(Kb, S);
-    vs.load(Vb, S);
-    ks.store(smem, 1.f);
-    vs.store(smem + TILE, 1.f);
+    const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
+    ks.load(0);
+    vs.load(0);
+    ks.store(smem, 1.f, tid);
+    vs.store(smem + TILE, 1.f, tid);
     __syncthreads();
 
     // two tiles per trip so every LDS buffer offset is a compile-time immediate
@@ -310,26 +310,28 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         {
             const bool more = j + 1 < ntiles;
             if (more) {
-                ks.load(Kb + (long)(j + 1) * KT * D, S - (j + 1) * KT);
-                vs.load(Vb + (long)(j + 1) * KT * D, S - (j + 1) * KT);
+                ks.load((j + 1) * KT);
+                vs.load((j + 1) * KT);
             }
-            fwd_tile<D>(st, smem, smem + TILE, fo, j * KT, S, h);
+            if (j == last_ragged) fwd_tile<D, true>(st, smem, smem + TILE, fo, j * KT, S, h);
+            else fwd_tile<D, false>(st, smem, smem + TILE, fo, j * KT, S, h);
             if (more) {
-                ks.store(smem + 2 * TILE, 1.f);
-                vs.store(smem + 3 * TILE, 1.f);
+                ks.store(smem + 2 * TILE, 1.f, tid);
+                vs.store(smem + 3 * TILE, 1.f, tid);
             }
             __syncthreads();
         }
         if (j + 1 < ntiles) {
             const bool more = j + 2 < ntiles;
             if (more) {
-                ks.load(Kb + (long)(j + 2) * KT * D, S - (j + 2) * KT);
-                vs.load(Vb + (long)(j + 2) * KT * D, S - (j + 2) * KT);
+                ks.load((j + 2) * KT);
+                vs.load((j + 2) * KT);
             }
-            fwd_tile<D>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
+            if (j + 1 == last_ragged) fwd_tile<D, true>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
+            else fwd_tile<D, false>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
             if (more) {
-                ks.store(smem, 1.f);
-                vs.store(smem + TILE, 1.f);
+                ks.store(smem, 1.f, tid);
+                vs.store(smem + TILE, 1.f, tid);
             }
             __syncthreads();
         }
@@ -356,16 +358,23 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
 #ifndef CUPY_INLINE_COMPILE
 namespace fa2 {
 
-template <int D>
-static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
-                                   hipStream_t stream) {
-    constexpr int NW = 4;
+template <int D, int NW>
+static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
+                                 hipStream_t stream) {
     const int nqb = (S + 32 * NW - 1) / (32 * NW);
     const long grid = (long)bh * nqb;
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k, v, o,
                        lse, S);
     return hipGetLastError();
+}
+
+template <int D>
+static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
+                                   hipStream_t stream) {
+    const int nw = tune_knob("FWD_WAVES", 8);
+    if (nw == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
+    return fwd_f16_launch<D, 4>(q, k, v, o, lse, bh, S, stream);
 }
 
 hipError_t launch_forward_f16(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,

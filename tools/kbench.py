@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""A/B kernel variants in ONE process (guide §5.4 rule 24): interleaved rounds,
+median and min per variant.  Variants are FA2_TUNE_* environment settings read
+by the launchers at every launch.
+
+  python tools/kbench.py --shape 4,16,2048,64 --kernel fwd --variant FWD_WAVES=4 --variant FWD_WAVES=8
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cuda-flash-attention_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="4,16,2048,64")
+    ap.add_argument("--kernel", action="append", default=None, help="fwd|dkdv|dq|delta|bwd (repeatable)")
+    ap.add_argument("--variant", action="append", default=[], help="KNOB=V[,KNOB=V] (repeatable)")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    import fa2amd
+
+    B, H, S, D = (int(x) for x in args.shape.split(","))
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(42)
+    q, k, v = (torch.rand(B, H, S, D, generator=g).to(dev) for _ in range(3))
+    do = torch.randn(B, H, S, D, generator=g).to(dev)
+    o, lse = fa2amd.forward(q, k, v, "fp16")
+    dl = fa2amd.delta(do, o)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
+    flops = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "delta": 0.0, "bwd": 10.0}
+    calls = {
+        "fwd": lambda: fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
+        "dkdv": lambda: fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv),
+        "dq": lambda: fa2amd.backward_dq(q, k, v, do, lse, dl, dq),
+        "delta": lambda: fa2amd.delta(do, o, out=dl),
+        "bwd": lambda: fa2amd.backward(q, k, v, o, do, lse, "fp16", dq=dq, dk=dk, dv=dv, delta_buf=dl),
+    }
+    kernels = args.kernel or ["fwd", "dkdv", "dq"]
+    variants = args.variant or [""]
+
+    def setenv(var):
+        for key in list(os.environ):
+            if key.startswith("FA2_TUNE_"):
+                del os.environ[key]
+        for kv in filter(None, var.split(",")):
+            kk, vv = kv.split("=")
+            os.environ["FA2_TUNE_" + kk] = vv
+
+    res = {(kn, var): [] for kn in kernels for var in variants}
+    for r in range(args.rounds):
+        for var in variants:
+            setenv(var)
+            for kn in kernels:
+                f = calls[kn]
+                f()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    f()
+                e1.record()
+                e1.synchronize()
+                res[(kn, var)].append(e0.elapsed_time(e1) / args.iters)
+    out = []
+    for (kn, var), ts in res.items():
+        med, mn = statistics.median(ts), min(ts)
+        tf = flops[kn] * B * H * S * S * D / (med * 1e-3) / 1e12
+        out.append({"kernel": kn, "variant": var or "default", "median_ms": round(med, 4), "min_ms": round(mn, 4),
+                    "tflops_alg": round(tf, 1)})
+        print(f"{kn:6s} {var or 'default':28s} median {med:8.4f} ms  min {mn:8.4f}  {tf:7.1f} TF(alg)")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,25 @@
+#!/bin/bash
+# rocprofv3 PMC passes over a short bench run (one counter group per pass, no
+# tracing domains combined with --pmc).  Output: gpurun_out/pmc/<pass>/...
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/pmc
+mkdir -p $OUT
+ARGS="${BENCH_ARGS:---steps 5 --warmup 2 --no-cpu-baseline}"
+PASSES=(
+  "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_VALU_TRANS_F32 SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
+  "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY"
+  "FETCH_SIZE GRBM_GUI_ACTIVE"
+  "WRITE_SIZE SQ_LDS_UNALIGNED_STALL SQ_ACTIVE_INST_ANY"
+)
+i=0
+for p in "${PASSES[@]}"; do
+  i=$((i+1))
+  echo "== pass $i: $p" >> $OUT/status.txt
+  timeout -k 10 300 rocprofv3 --pmc $p -d $OUT/p$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1
+  rc=$?
+  echo "pass $i rc=$rc" >> $OUT/status.txt
+  [ $rc -ne 0 ] && exit $rc
+done
+python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1
+echo done >> $OUT/status.txt
