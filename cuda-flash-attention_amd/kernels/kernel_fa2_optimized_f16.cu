@@ -256,6 +256,164 @@ __device__ __forceinline__ void fwd_tile(FwdState<D>& st, const _Float16* Ks, co
             for (int s = 0; s < 2; ++s) st.oacc[b] = mfma(fo.trop(Vs, kb * 32 + 16 * s, b), pf[kb][s], st.oacc[b]);
 }
 
+// ---- software-pipelined forward (guide T15): S^T of tile j+1 is issued on the
+// MFMA pipe before the softmax of tile j runs on the VALU, so the two overlap
+// inside one wave; K is staged two tiles ahead, V one.
+template <int D>
+__device__ __forceinline__ void fwd_qk(f32x16 (&s)[2], const FwdState<D>& st, const _Float16* Ks,
+                                       const FragOffsets<D>& fo) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) s[kb] = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], s[kb]);
+    }
+}
+
+template <int D, bool MASK>
+__device__ __forceinline__ void fwd_softmax_pv(FwdState<D>& st, f32x16 (&sacc)[2], const _Float16* Vs,
+                                               const FragOffsets<D>& fo, int k0, int S, int h) {
+    if (MASK) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[kb][i] = -__builtin_inff();
+    }
+    float mx = fmaxf(sacc[0][0], sacc[0][1]);
+#pragma unroll
+    for (int i = 2; i < 16; ++i) mx = fmaxf(mx, sacc[0][i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[1][i]);
+    mx = xor32_max(mx);
+    const bool grow = mx > st.m + FA2_RESCALE_THR;
+    if (__any(grow)) {
+        const float mnew = grow ? mx : st.m;
+        const float alpha = fast_exp2(st.m - mnew);
+        st.m = mnew;
+        st.l *= alpha;
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) st.oacc[b][i] *= alpha;
+    }
+    f16x8 pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float p = fast_exp2(sacc[kb][i] - st.m);
+            st.l += p;
+            pf[kb][i >> 3][i & 7] = (_Float16)p;
+        }
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) st.oacc[b] = mfma(fo.trop(Vs, kb * 32 + 16 * s, b), pf[kb][s], st.oacc[b]);
+}
+
+template <int D, int NW>
+__global__ void __launch_bounds__(64 * NW)
+fa2_fwd_f16_pipe_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                        float* __restrict__ O, float* __restrict__ LSE, int S) {
+    constexpr int KT = 64;
+    constexpr int NT = 64 * NW;
+    constexpr int TILE = KT * D;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * TILE];  // K0 K1 V0 V1
+    _Float16* const Kb0 = smem;
+    _Float16* const Kb1 = smem + TILE;
+    _Float16* const Vb0 = smem + 2 * TILE;
+    _Float16* const Vb1 = smem + 3 * TILE;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int nqb = (S + 32 * NW - 1) / (32 * NW);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = bid / nqb, qb = bid - bh * nqb;
+    const long base = (long)bh * S * D;
+    const int q = qb * 32 * NW + wave * 32 + r;
+    const float qscale = FA2_LOG2E / __builtin_sqrtf((float)D);
+
+    FwdState<D> st;
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+        if (q < S) {
+            const f32x4* p = reinterpret_cast<const f32x4*>(Q + base + (long)q * D + 16 * t + 8 * h);
+            st.qf[t] = to_f16x8(p[0], p[1], qscale);
+        } else {
+            st.qf[t] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) st.oacc[b][i] = 0.f;
+    st.m = -__builtin_inff();
+    st.l = 0.f;
+
+    FragOffsets<D> fo;
+    fo.init(lane);
+    TileStager<D, KT, NT> ks, vs;
+    ks.init(K + base, S, tid);
+    vs.init(V + base, S, tid);
+    const int nt = (S + KT - 1) / KT;
+    const int last_ragged = (S % KT) ? nt - 1 : -1;
+
+    // prologue: K0, V0 -> LDS; S_0; K1 -> LDS
+    ks.load(0);
+    vs.load(0);
+    ks.store(Kb0, 1.f, tid);
+    vs.store(Vb0, 1.f, tid);
+    if (nt > 1) ks.load(KT);
+    __syncthreads();
+    f32x16 sA[2], sB[2];
+    fwd_qk<D>(sA, st, Kb0, fo);
+    if (nt > 1) ks.store(Kb1, 1.f, tid);
+    __syncthreads();
+
+    for (int j = 0; j < nt; j += 2) {
+        {  // step j: S_j in sA, K_{j+1} in Kb1, V_j in Vb0
+            const bool hn = j + 1 < nt, hnn = j + 2 < nt;
+            if (hn) vs.load((j + 1) * KT);
+            if (hnn) ks.load((j + 2) * KT);
+            if (hn) fwd_qk<D>(sB, st, Kb1, fo);
+            if (j == last_ragged) fwd_softmax_pv<D, true>(st, sA, Vb0, fo, j * KT, S, h);
+            else fwd_softmax_pv<D, false>(st, sA, Vb0, fo, j * KT, S, h);
+            if (hn) vs.store(Vb1, 1.f, tid);
+            if (hnn) ks.store(Kb0, 1.f, tid);
+            __syncthreads();
+        }
+        if (j + 1 < nt) {  // step j+1: S in sB, K_{j+2} in Kb0, V_{j+1} in Vb1
+            const bool hn = j + 2 < nt, hnn = j + 3 < nt;
+            if (hn) vs.load((j + 2) * KT);
+            if (hnn) ks.load((j + 3) * KT);
+            if (hn) fwd_qk<D>(sA, st, Kb0, fo);
+            if (j + 1 == last_ragged) fwd_softmax_pv<D, true>(st, sB, Vb1, fo, (j + 1) * KT, S, h);
+            else fwd_softmax_pv<D, false>(st, sB, Vb1, fo, (j + 1) * KT, S, h);
+            if (hn) vs.store(Vb0, 1.f, tid);
+            if (hnn) ks.store(Kb1, 1.f, tid);
+            __syncthreads();
+        }
+    }
+
+    const float lt = xor32_sum(st.l);
+    const float inv = 1.f / lt;
+    if (q < S) {
+        float* orow = O + base + (long)q * D;
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 v = {st.oacc[b][4 * g] * inv, st.oacc[b][4 * g + 1] * inv, st.oacc[b][4 * g + 2] * inv,
+                           st.oacc[b][4 * g + 3] * inv};
+                *reinterpret_cast<f32x4*>(orow + 32 * b + 8 * g + 4 * h) = v;
+            }
+        if (h == 0) LSE[(long)bh * S + q] = st.m * FA2_LN2 + __logf(lt);
+    }
+}
+
 // Grid: BH * ceil(S / (32*NW)) workgroups of 64*NW threads (NW waves x 32 queries).
 template <int D, int NW>
 __global__ void __launch_bounds__(64 * NW)
@@ -364,15 +522,19 @@ static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v,
     const int nqb = (S + 32 * NW - 1) / (32 * NW);
     const long grid = (long)bh * nqb;
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k, v, o,
-                       lse, S);
+    if (tune_knob("FWD_PIPE", D <= 64 ? 1 : 0))
+        hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_pipe_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream,
+                           q, k, v, o, lse, S);
+    else
+        hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
+                           v, o, lse, S);
     return hipGetLastError();
 }
 
 template <int D>
 static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
                                    hipStream_t stream) {
-    const int nw = tune_knob("FWD_WAVES", 8);
+    const int nw = tune_knob("FWD_WAVES", D <= 64 ? 8 : 4);
     if (nw == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
     return fwd_f16_launch<D, 4>(q, k, v, o, lse, bh, S, stream);
 }
