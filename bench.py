@@ -50,16 +50,30 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def traffic_from_profile(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_summary.json, written by tools/pmc_summary.py), or None."""
+PMC_PREFIX = {"fwd": "fa2_fwd_f16", "dkdv": "fa2_bwd_dkdv_f16", "dq": "fa2_bwd_dq_f16", "delta": "fa2_delta",
+              "bwd": "fa2_bwd_f32"}
+
+
+def traffic_from_profile(kernel: str, D: int, S: int, heads: int):
+    """HBM bytes per launch of `kernel` (FETCH_SIZE x 2 + WRITE_SIZE, gfx950-corrected)
+    from the committed rocprofv3 PMC summary profiles/pmc_summary.json (tools/pmc.sh ->
+    tools/pmc_summary.py), or None when it does not cover this kernel and shape."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
-            ent = json.load(f).get(kernel)
-        return None if ent is None else float(ent["hbm_bytes_per_launch"])
-    except (OSError, ValueError, KeyError, TypeError):
+            summ = json.load(f)
+    except (OSError, ValueError):
         return None
+    meta = summ.get("_meta", {})
+    if meta and (meta.get("S") != S or meta.get("D") != D or meta.get("heads") != heads):
+        return None
+    for name, ent in summ.items():
+        if name.startswith(PMC_PREFIX.get(kernel, "?")) and (f"<{D}," in name or f"<{D}>" in name):
+            try:
+                return float(ent["hbm_bytes_per_launch"])
+            except (KeyError, TypeError):
+                return None
+    return None
 
 
 def cpu_baseline(S, D, sample_heads=None):
@@ -183,7 +197,7 @@ def main():
     peak = MFMA_F16_PEAK_TFLOPS if prec == "fp16" else MFMA_F32_PEAK_TFLOPS
     achieved = dom_flops / (kms[dom] * 1e-3) / 1e12
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic_from_profile(dom),
+            "frac": round(achieved / peak, 4), "traffic": traffic_from_profile(dom, D, S, heads),
             "kernel_ms": {n: round(x, 4) for n, x in kms.items()}}
 
     cpu = None

@@ -21,5 +21,5 @@ for p in "${PASSES[@]}"; do
   echo "pass $i rc=$rc" >> $OUT/status.txt
   [ $rc -ne 0 ] && exit $rc
 done
-python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1
+PMC_META='{"S": 2048, "D": 64, "heads": 64, "workload": "B4_H16_S2048_D64 fp16, bench.py --steps 5 --warmup 2", "source": "tools/pmc.sh"}' python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1
 echo done >> $OUT/status.txt

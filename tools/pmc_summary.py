@@ -56,10 +56,15 @@ def main():
                 if c in m:
                     e[c.lower() + "_frac"] = m[c] / m["SQ_WAVE_CYCLES"]
         out[k] = e
+    meta = os.environ.get("PMC_META")
+    if meta:
+        out["_meta"] = json.loads(meta)
     text = json.dumps(out, indent=1, sort_keys=True)
     with open(os.path.join(d, "pmc_summary.json"), "w") as f:
         f.write(text)
     for k, e in out.items():
+        if k.startswith("_"):
+            continue
         print(k)
         for n, v in sorted(e.items()):
             if n != "counters":
