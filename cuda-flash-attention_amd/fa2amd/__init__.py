@@ -49,6 +49,18 @@ def build(jobs: int = 8) -> str:
     return LIB_PATH
 
 
+_libs = {}
+
+
+def use_library(path: str):
+    """Switch the active extension to another build of the same C ABI (tools/kbench.py
+    A/B's compiler-flag variants in one process this way)."""
+    global _lib
+    _lib = _libs.get(path) or _load(path)
+    _libs[path] = _lib
+    return _lib
+
+
 def lib():
     """Load lib/libfa2amd.so (raises FA2Error if it was not built)."""
     global _lib
@@ -56,7 +68,12 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise FA2Error(f"HIP extension not built: {LIB_PATH} is missing (run __graft_entry__.build())")
-    L = ctypes.CDLL(LIB_PATH)
+    _lib = _load(LIB_PATH)
+    return _lib
+
+
+def _load(path):
+    L = ctypes.CDLL(path)
     P, I, V = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p
     FP = ctypes.POINTER(ctypes.c_float)
     sig = {
@@ -76,7 +93,6 @@ def lib():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = ctypes.c_char_p if name == "fa2_last_error" else I
-    _lib = L
     return L
 
 

@@ -173,57 +173,92 @@ struct TileStager {
 // ---------------------------------------------------------------------------
 // dK, dV:  grid BH * ceil(S / (32*NW)), block 64*NW
 // ---------------------------------------------------------------------------
-template <int D>
+template <int D, int KB>
 struct DkdvState {
-    f16x8 kf[D / 16], vf[D / 16];  // B operands: this lane's key row of K (scaled) and V
-    f32x16 dka[D / 32], dva[D / 32];
+    // KB blocks of 32 keys per wave: B operands (this lane's key rows of K, scaled, and V)
+    f16x8 kf[KB][D / 16], vf[KB][D / 16];
+    f32x16 dka[KB][D / 32], dva[KB][D / 32];
 };
 
-// One 64-query step: S = Q K^T and dP = dO V^T with the key on the lane (their
-// accumulators start at -LSE*log2e and -Delta), P = exp2(S), dS = P*(dP - Delta),
-// then dV^T += dO^T P and dK^T += Q^T dS with P / dS packed as B operands.
-template <int D>
-__device__ __forceinline__ void dkdv_step(DkdvState<D>& st, const _Float16* Qs, const _Float16* dOs,
+// One 64-query step for the wave's KB x 32 keys: S = Q K^T and dP = dO V^T with the
+// key on the lane (their accumulators start at -LSE*log2e and -Delta), P = exp2(S),
+// dS = P*(dP - Delta), then dV^T += dO^T P and dK^T += Q^T dS with P / dS packed as
+// B operands.  Every LDS fragment (Q / dO rows, dO^T / Q^T columns) feeds KB MFMAs.
+// ABL (timing ablations only, tools/kbench.py; results are wrong when set):
+//   2 = no softmax VALU, 8 = no dV/dK MFMAs, 16 = no S/dP MFMAs
+template <int D, int KB, int ABL = 0>
+__device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* Qs, const _Float16* dOs,
                                           const float* nlse2, const float* ndel, const FragOffsets<D>& fo, int h) {
-    f16x8 pf[2][2], dsf[2][2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
         // accumulator rows: query qb*32 + (i&3) + 8*(i>>2) + 4h ; col: key (lane)
-        f32x16 sa, da;
+        f32x16 init_s, init_d;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const f32x4 lv = *reinterpret_cast<const f32x4*>(nlse2 + qb * 32 + 8 * g + 4 * h);
             const f32x4 dv = *reinterpret_cast<const f32x4*>(ndel + qb * 32 + 8 * g + 4 * h);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                sa[4 * g + e] = lv[e];
-                da[4 * g + e] = dv[e];
+                init_s[4 * g + e] = lv[e];
+                init_d[4 * g + e] = dv[e];
             }
         }
+        f32x16 sa[KB], da[KB];
 #pragma unroll
-        for (int t = 0; t < D / 16; ++t) {
-            sa = mfma(fo.rowop(Qs, qb * 32, t), st.kf[t], sa);
-            da = mfma(fo.rowop(dOs, qb * 32, t), st.vf[t], da);
+        for (int kb = 0; kb < KB; ++kb) {
+            sa[kb] = init_s;
+            da[kb] = init_d;
         }
+        if (!(ABL & 16)) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float p = fast_exp2(sa[i]);
-            pf[qb][i >> 3][i & 7] = (_Float16)p;
-            dsf[qb][i >> 3][i & 7] = (_Float16)(p * da[i]);
+            for (int t = 0; t < D / 16; ++t) {
+                const f16x8 qa = fo.rowop(Qs, qb * 32, t), da_op = fo.rowop(dOs, qb * 32, t);
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb) {
+                    sa[kb] = mfma(qa, st.kf[kb][t], sa[kb]);
+                    da[kb] = mfma(da_op, st.vf[kb][t], da[kb]);
+                }
+            }
         }
-    }
+        f16x8 pf[KB][2], dsf[KB][2];
 #pragma unroll
-    for (int b = 0; b < D / 32; ++b)
+        for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
+            for (int i = 0; i < 16; ++i) {
+                if (ABL & 2) {
+                    pf[kb][i >> 3][i & 7] = (_Float16)sa[kb][i];
+                    dsf[kb][i >> 3][i & 7] = (_Float16)da[kb][i];
+                } else {
+                    const float p = fast_exp2(sa[kb][i]);
+                    pf[kb][i >> 3][i & 7] = (_Float16)p;
+                    dsf[kb][i >> 3][i & 7] = (_Float16)(p * da[kb][i]);
+                }
+            }
+        if (ABL & 8) {
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(pf[kb][s]), "v"(dsf[kb][s]));
+            continue;
+        }
+        // dV^T += dO^T P ; dK^T += Q^T dS over this query block's 32 rows
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                st.dva[b] = mfma(fo.trop(dOs, qb * 32 + 16 * s, b), pf[qb][s], st.dva[b]);
-                st.dka[b] = mfma(fo.trop(Qs, qb * 32 + 16 * s, b), dsf[qb][s], st.dka[b]);
+                const f16x8 a_do = fo.trop(dOs, qb * 32 + 16 * s, b), a_q = fo.trop(Qs, qb * 32 + 16 * s, b);
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb) {
+                    st.dva[kb][b] = mfma(a_do, pf[kb][s], st.dva[kb][b]);
+                    st.dka[kb][b] = mfma(a_q, dsf[kb][s], st.dka[kb][b]);
+                }
             }
+    }
 }
 
-template <int D, int NW>
+// KB x 32 keys per wave, NW waves: grid BH * ceil(S / (32*KB*NW)), block 64*NW.
+// ABL: timing ablations (see dkdv_step; plus 1 = no staging in the loop, 4 = no barrier)
+template <int D, int NW, int KB = 1, int ABL = 0>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                         const float* __restrict__ dO, const float* __restrict__ LSE,
@@ -231,50 +266,63 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     constexpr int QT = 64;  // query rows per step
     constexpr int NT = 64 * NW;
     constexpr int TILE = QT * D;
+    constexpr int KPW = 32 * KB;  // keys per wave
     // [buf][Q | dO] fp16 tiles, then [buf][-lse2 | -delta] fp32 rows
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
     __shared__ __attribute__((aligned(16))) float rows[2][2][QT];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int nkb = (S + 32 * NW - 1) / (32 * NW);
+    const int nkb = (S + KPW * NW - 1) / (KPW * NW);
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = bid / nkb, kb = bid - bh * nkb;
+    const int bh = bid / nkb, kblk = bid - bh * nkb;
     const long base = (long)bh * S * D;
     const long rbase = (long)bh * S;
-    const int key = kb * 32 * NW + wave * 32 + r;
-    const bool kvalid = key < S;
+    const int key0 = kblk * KPW * NW + wave * KPW;  // this wave's first key
     const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
 
-    DkdvState<D> st;
+    DkdvState<D, KB> st;
 #pragma unroll
-    for (int t = 0; t < D / 16; ++t) {
-        st.kf[t] = load_frag(K + base + (long)key * D + 16 * t + 8 * h, kvalid, kscale);
-        st.vf[t] = load_frag(V + base + (long)key * D + 16 * t + 8 * h, kvalid, 1.f);
-    }
+    for (int kb = 0; kb < KB; ++kb) {
+        const int key = key0 + kb * 32 + r;
 #pragma unroll
-    for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            st.dka[b][i] = 0.f;
-            st.dva[b][i] = 0.f;
+        for (int t = 0; t < D / 16; ++t) {
+            st.kf[kb][t] = load_frag(K + base + (long)key * D + 16 * t + 8 * h, key < S, kscale);
+            st.vf[kb][t] = load_frag(V + base + (long)key * D + 16 * t + 8 * h, key < S, 1.f);
         }
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                st.dka[kb][b][i] = 0.f;
+                st.dva[kb][b][i] = 0.f;
+            }
+    }
 
     FragOffsets<D> fo;
     fo.init(lane);
     TileStager<D, QT, NT> qs, dos;
     qs.init(Q + base, S, tid);
     dos.init(dO + base, S, tid);
-    float rowv = 0.f;  // -lse2 (threads [0,QT)) or -delta (threads [QT,2QT)) of the staged step
+    // Row constants of the staged step: wave 0 carries LSE, wave 1 carries Delta
+    // (QT == 64 == one wave).  Loaded raw by a range-checked buffer load (rows >= S
+    // read 0) and only scaled / negated / masked at store time, so nothing waits on
+    // the load before the step's MFMAs (a guarded global load there made the
+    // compiler drain vmcnt -- the K/V staging loads too -- at every step start).
+    static_assert(QT == 64, "one wave per row vector");
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const __amdgpu_buffer_rsrc_t rs_lse = head_rsrc(LSE + rbase, S, 1);
+    const __amdgpu_buffer_rsrc_t rs_del = head_rsrc(Delta + rbase, S, 1);
+    float rowraw = 0.f;
+    int rowq = 0;
     auto load_rows = [&](int q0) {
-        if (tid < 2 * QT) {
-            const int qi = q0 + (tid & (QT - 1));
-            // stored negated: they are the initial accumulators of S and dP
-            if (tid < QT) rowv = qi < S ? -LSE[rbase + qi] * FA2B_LOG2E : -__builtin_inff();
-            else rowv = qi < S ? -Delta[rbase + qi] : 0.f;
-        }
+        rowq = q0 + lane;
+        if (wave_u == 0) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
+        else if (wave_u == 1) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_del, lane * 4, q0 * 4, 0));
     };
     auto store_rows = [&](int buf) {
-        if (tid < 2 * QT) rows[buf][tid / QT][tid & (QT - 1)] = rowv;
+        // stored negated: they are the initial accumulators of S and dP
+        if (wave_u == 0) rows[buf][0][lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
+        else if (wave_u == 1) rows[buf][1][lane] = -rowraw;
     };
     auto load_step = [&](int it) {
         qs.load(it * QT);
@@ -291,43 +339,48 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
 
     for (int it = 0; it < nsteps; it += 2) {
         {
-            const bool more = it + 1 < nsteps;
+            const bool more = !(ABL & 1) && it + 1 < nsteps;
             if (more) load_step(it + 1);
-            dkdv_step<D>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h);
+            dkdv_step<D, KB, ABL>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h);
             if (more) {
                 qs.store(smem + 2 * TILE, 1.f, tid);
                 dos.store(smem + 3 * TILE, 1.f, tid);
                 store_rows(1);
             }
-            __syncthreads();
+            if (!(ABL & 4)) __syncthreads();
         }
         if (it + 1 < nsteps) {
-            const bool more = it + 2 < nsteps;
+            const bool more = !(ABL & 1) && it + 2 < nsteps;
             if (more) load_step(it + 2);
-            dkdv_step<D>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h);
+            dkdv_step<D, KB, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h);
             if (more) {
                 qs.store(smem, 1.f, tid);
                 dos.store(smem + TILE, 1.f, tid);
                 store_rows(0);
             }
-            __syncthreads();
+            if (!(ABL & 4)) __syncthreads();
         }
     }
 
-    if (kvalid) {
-        const float dscale = 1.f / __builtin_sqrtf((float)D);
-        float* dkrow = dK + base + (long)key * D;
-        float* dvrow = dV + base + (long)key * D;
+    const float dscale = 1.f / __builtin_sqrtf((float)D);
 #pragma unroll
-        for (int b = 0; b < D / 32; ++b)
+    for (int kb = 0; kb < KB; ++kb) {
+        const int key = key0 + kb * 32 + r;
+        if (key < S) {
+            float* dkrow = dK + base + (long)key * D;
+            float* dvrow = dV + base + (long)key * D;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                f32x4 a = {st.dka[b][4 * g] * dscale, st.dka[b][4 * g + 1] * dscale, st.dka[b][4 * g + 2] * dscale,
-                           st.dka[b][4 * g + 3] * dscale};
-                f32x4 c = {st.dva[b][4 * g], st.dva[b][4 * g + 1], st.dva[b][4 * g + 2], st.dva[b][4 * g + 3]};
-                *reinterpret_cast<f32x4*>(dkrow + 32 * b + 8 * g + 4 * h) = a;
-                *reinterpret_cast<f32x4*>(dvrow + 32 * b + 8 * g + 4 * h) = c;
-            }
+            for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x16& ka = st.dka[kb][b];
+                    const f32x16& va = st.dva[kb][b];
+                    f32x4 a = {ka[4 * g] * dscale, ka[4 * g + 1] * dscale, ka[4 * g + 2] * dscale, ka[4 * g + 3] * dscale};
+                    f32x4 c = {va[4 * g], va[4 * g + 1], va[4 * g + 2], va[4 * g + 3]};
+                    *reinterpret_cast<f32x4*>(dkrow + 32 * b + 8 * g + 4 * h) = a;
+                    *reinterpret_cast<f32x4*>(dvrow + 32 * b + 8 * g + 4 * h) = c;
+                }
+        }
     }
 }
 
@@ -477,20 +530,42 @@ namespace fa2 {
 namespace {
 // waves per workgroup: 8 x 32 keys for D <= 64 (2 waves/SIMD fit in 256 VGPRs);
 // D = 128 needs more than 256 registers per lane, so 4 waves (1 per SIMD).
-template <int D, int NW>
+template <int D, int NW, int KB = 1, int ABL = 0>
 hipError_t dkdv_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                        const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-    const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
+    const long grid = (long)bh * ((S + 32 * KB * NW - 1) / (32 * KB * NW));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream,
-                       q, k, v, dout, lse, delta, dk, dv, S);
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, KB, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0,
+                       stream, q, k, v, dout, lse, delta, dk, dv, S);
     return hipGetLastError();
 }
+// Geometry (FA2_TUNE_DKDV_WAVES / FA2_TUNE_DKDV_KB): 8 waves x 32 keys for D <= 64
+// (2 waves/SIMD in 256 VGPRs), or 4 waves x 64 keys (1 wave/SIMD, 512 registers,
+// every LDS fragment feeding two MFMAs); D = 128 always 4 x 32.
 template <int D>
 hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                          const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
     const int nw = tune_knob("DKDV_WAVES", D <= 64 ? 8 : 4);
-    if (nw == 8 && D <= 64) return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+    const int kbk = tune_knob("DKDV_KB", 1);
+#ifdef FA2_ABLATIONS
+    if constexpr (D == 64) {
+        if (nw == 8) switch (tune_knob("DKDV_ABL", 0)) {
+            case 1: return dkdv_launch<D, 8, 1, 1>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+            case 2: return dkdv_launch<D, 8, 1, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+            case 4: return dkdv_launch<D, 8, 1, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+            case 8: return dkdv_launch<D, 8, 1, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+            case 16: return dkdv_launch<D, 8, 1, 16>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+            default: break;
+        }
+    }
+#endif
+    if constexpr (D <= 64) {
+        if (kbk == 2) {
+            if (D == 32 && nw == 8) return dkdv_launch<D, 8, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+            return dkdv_launch<D, 4, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        }
+        if (nw == 8) return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+    }
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
 template <int D, int NW>

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--variant", action="append", default=[], help="KNOB=V[,KNOB=V] (repeatable)")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--lib", action="append", default=[], help="alternate libfa2amd.so builds to A/B (repeatable)")
     args = ap.parse_args()
     import torch
     import fa2amd
@@ -44,12 +45,20 @@ def main():
     }
     kernels = args.kernel or ["fwd", "dkdv", "dq"]
     variants = args.variant or [""]
+    libs = args.lib or [None]
+    if args.lib:
+        variants = [f"lib={l}" + ("," + v if v else "") for l in libs for v in (args.variant or [""])]
 
     def setenv(var):
+        if var.startswith("lib="):
+            path, _, var = var[4:].partition(",")
+            fa2amd.use_library(path)
         for key in list(os.environ):
             if key.startswith("FA2_TUNE_"):
                 del os.environ[key]
         for kv in filter(None, var.split(",")):
+            if kv.startswith("lib="):
+                continue
             kk, vv = kv.split("=")
             os.environ["FA2_TUNE_" + kk] = vv
 
