@@ -150,8 +150,9 @@ struct TileStager {
     int voff[CPT], loff[CPT];
     __amdgpu_buffer_rsrc_t rs;
 
+    __device__ __forceinline__ void set_head(const float* head_base, int S) { rs = head_rsrc(head_base, S, D); }
     __device__ __forceinline__ void init(const float* head_base, int S, int tid) {
-        rs = head_rsrc(head_base, S, D);
+        set_head(head_base, S);
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
             const int x = tid + c * NT;
@@ -190,31 +191,96 @@ __device__ __forceinline__ float xor32_sum(float x) {
 // forward
 // ---------------------------------------------------------------------------
 // Online-softmax state of one wave: 32 query rows (one per lane pair), O^T
-// accumulator (d on the rows), running max m (log2 domain) and per-half sum l.
+// accumulator (d on the rows), running max m (log2 domain), per-half sum l, and
+// nm = -m broadcast over 16 registers: the initial value of every S^T
+// accumulator, so the QK^T MFMAs produce s - m directly (no per-score v_sub).
+// pend: shift not yet applied to an S^T tile that was issued before m last moved
+// (software pipelining; 0 almost always).
 template <int D>
 struct FwdState {
     f16x8 qf[D / 16];
     f32x16 oacc[D / 32];
-    float m, l;
+    f32x16 nm;
+    float m, pend;
+    float l[4];  // four partial row sums: four short dependency chains per tile, not one of 32
 };
 
 // Lazy rescale (guide T13): the running max moves only when a tile's max
 // exceeds it by more than RESCALE_THR (log2 units), so p <= 2^8 in fp16/fp32.
 #define FA2_RESCALE_THR 8.0f
 
-// One 64-key tile: S^T = K Q^T (keys on registers, query on the lane), online
-// softmax, O^T += V^T P^T with the packed S^T accumulator as B operand.
-template <int D, bool MASK>
-__device__ __forceinline__ void fwd_tile(FwdState<D>& st, const _Float16* Ks, const _Float16* Vs,
-                                         const FragOffsets<D>& fo, int k0, int S, int h) {
-    f32x16 sacc[2];
+// -m as one opaque 16-register tuple: without the empty asm the compiler
+// rematerialises the splat with 16 v_mov before every QK^T chain.
+__device__ __forceinline__ f32x16 splat16(float x) {
+    f32x16 v = x;
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// S^T of one 64-key tile (keys on registers, query on the lane), relative to m.
+template <int D, int ABL = 0>
+__device__ __forceinline__ void fwd_qk(f32x16 (&s)[2], const FwdState<D>& st, const _Float16* Ks,
+                                       const FragOffsets<D>& fo) {
+    if (ABL & 16) {
+        s[0] = st.nm + fo.rowop(Ks, 0, 0)[0];
+        s[1] = st.nm;
+        return;
+    }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+        s[kb] = mfma(fo.rowop(Ks, kb * 32, 0), st.qf[0], st.nm);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
-#pragma unroll
-        for (int t = 0; t < D / 16; ++t) sacc[kb] = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], sacc[kb]);
+        for (int t = 1; t < D / 16; ++t) s[kb] = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], s[kb]);
     }
+}
+
+// Row max of a 32-score register tile as four independent max3 chains.
+__device__ __forceinline__ float tile_max(const f32x16 (&t)[2]) {
+    float c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        c[k] = fmaxf(t[0][k], t[0][k + 4]);
+        c[k] = fmaxf(fmaxf(c[k], t[0][k + 8]), t[0][k + 12]);
+        c[k] = fmaxf(fmaxf(c[k], t[1][k]), t[1][k + 4]);
+        c[k] = fmaxf(fmaxf(c[k], t[1][k + 8]), t[1][k + 12]);
+    }
+    return fmaxf(fmaxf(c[0], c[1]), fmaxf(c[2], c[3]));
+}
+
+// p = exp2(s - m - sh) (sh = 0 on the common path), row sum, O^T += V^T P^T with
+// the packed scores as the B operand.
+template <int D, bool SHIFT, int ABL = 0>
+__device__ __forceinline__ void fwd_exp_pv(FwdState<D>& st, const f32x16 (&sacc)[2], float sh, const _Float16* Vs,
+                                           const FragOffsets<D>& fo) {
+    f16x8 pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float x = SHIFT ? sacc[kb][i] - sh : sacc[kb][i];
+            const float p = (ABL & 2) ? x : fast_exp2(x);
+            st.l[i & 3] += p;
+            pf[kb][i >> 3][i & 7] = (_Float16)p;
+        }
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                if (ABL & 8) st.oacc[b][s + 2 * kb] += (float)pf[kb][s][b];
+                else st.oacc[b] = mfma(fo.trop(Vs, kb * 32 + 16 * s, b), pf[kb][s], st.oacc[b]);
+            }
+}
+
+// Online softmax of one tile (sacc = s - m + pend).  The common path is exp + PV
+// only; when m moves (first tile: m := row max; later: a row max more than
+// RESCALE_THR above m) the slow path rescales l and O and shifts the scores.
+// NEXT: the next tile's scores were already issued against the old m, so they
+// carry the shift in pend.
+template <int D, bool MASK, bool NEXT, int ABL = 0>
+__device__ __forceinline__ void fwd_softmax_pv(FwdState<D>& st, f32x16 (&sacc)[2], const _Float16* Vs,
+                                               const FragOffsets<D>& fo, int k0, int S, int h, bool first) {
     if (MASK) {  // ragged last tile only
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
@@ -222,217 +288,41 @@ __device__ __forceinline__ void fwd_tile(FwdState<D>& st, const _Float16* Ks, co
             for (int i = 0; i < 16; ++i)
                 if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[kb][i] = -__builtin_inff();
     }
-    float mx = fmaxf(sacc[0][0], sacc[0][1]);
+    float mx = tile_max(sacc);
+    mx = xor32_max(mx) - st.pend;
+    if (ABL & 32) mx = sacc[0][0];
+    const bool grow = first || mx > FA2_RESCALE_THR;
+    if (__any(grow || st.pend != 0.f)) {
+        const float d = grow ? mx : 0.f;
+        const float alpha = first ? 0.f : fast_exp2(-d);
+        const float sh = st.pend + d;
+        st.m += d;
 #pragma unroll
-    for (int i = 2; i < 16; ++i) mx = fmaxf(mx, sacc[0][i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[1][i]);
-    mx = xor32_max(mx);
-    const bool grow = mx > st.m + FA2_RESCALE_THR;
-    if (__any(grow)) {
-        const float mnew = grow ? mx : st.m;
-        const float alpha = fast_exp2(st.m - mnew);
-        st.m = mnew;
-        st.l *= alpha;
+        for (int c = 0; c < 4; ++c) st.l[c] *= alpha;
 #pragma unroll
         for (int b = 0; b < D / 32; ++b)
 #pragma unroll
             for (int i = 0; i < 16; ++i) st.oacc[b][i] *= alpha;
+        st.nm = splat16(-st.m);
+        st.pend = NEXT ? d : 0.f;
+        fwd_exp_pv<D, true, ABL>(st, sacc, sh, Vs, fo);
+    } else {
+        fwd_exp_pv<D, false, ABL>(st, sacc, 0.f, Vs, fo);
     }
-    f16x8 pf[2][2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float p = fast_exp2(sacc[kb][i] - st.m);
-            st.l += p;
-            pf[kb][i >> 3][i & 7] = (_Float16)p;
-        }
-#pragma unroll
-    for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) st.oacc[b] = mfma(fo.trop(Vs, kb * 32 + 16 * s, b), pf[kb][s], st.oacc[b]);
 }
 
-// ---- software-pipelined forward (guide T15): S^T of tile j+1 is issued on the
-// MFMA pipe before the softmax of tile j runs on the VALU, so the two overlap
-// inside one wave; K is staged two tiles ahead, V one.
+// One 64-key tile, unpipelined: QK^T, then softmax and PV.
+template <int D, bool MASK, int ABL = 0>
+__device__ __forceinline__ void fwd_tile(FwdState<D>& st, const _Float16* Ks, const _Float16* Vs,
+                                         const FragOffsets<D>& fo, int k0, int S, int h, bool first) {
+    f32x16 sacc[2];
+    fwd_qk<D, ABL>(sacc, st, Ks, fo);
+    fwd_softmax_pv<D, MASK, false, ABL>(st, sacc, Vs, fo, k0, S, h, first);
+}
+
 template <int D>
-__device__ __forceinline__ void fwd_qk(f32x16 (&s)[2], const FwdState<D>& st, const _Float16* Ks,
-                                       const FragOffsets<D>& fo) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
-#pragma unroll
-        for (int t = 0; t < D / 16; ++t) s[kb] = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], s[kb]);
-    }
-}
-
-template <int D, bool MASK>
-__device__ __forceinline__ void fwd_softmax_pv(FwdState<D>& st, f32x16 (&sacc)[2], const _Float16* Vs,
-                                               const FragOffsets<D>& fo, int k0, int S, int h) {
-    if (MASK) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[kb][i] = -__builtin_inff();
-    }
-    float mx = fmaxf(sacc[0][0], sacc[0][1]);
-#pragma unroll
-    for (int i = 2; i < 16; ++i) mx = fmaxf(mx, sacc[0][i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[1][i]);
-    mx = xor32_max(mx);
-    const bool grow = mx > st.m + FA2_RESCALE_THR;
-    if (__any(grow)) {
-        const float mnew = grow ? mx : st.m;
-        const float alpha = fast_exp2(st.m - mnew);
-        st.m = mnew;
-        st.l *= alpha;
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) st.oacc[b][i] *= alpha;
-    }
-    f16x8 pf[2][2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float p = fast_exp2(sacc[kb][i] - st.m);
-            st.l += p;
-            pf[kb][i >> 3][i & 7] = (_Float16)p;
-        }
-#pragma unroll
-    for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) st.oacc[b] = mfma(fo.trop(Vs, kb * 32 + 16 * s, b), pf[kb][s], st.oacc[b]);
-}
-
-template <int D, int NW>
-__global__ void __launch_bounds__(64 * NW)
-fa2_fwd_f16_pipe_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                        float* __restrict__ O, float* __restrict__ LSE, int S) {
-    constexpr int KT = 64;
-    constexpr int NT = 64 * NW;
-    constexpr int TILE = KT * D;
-    __shared__ __attribute__((aligned(16))) _Float16 smem[4 * TILE];  // K0 K1 V0 V1
-    _Float16* const Kb0 = smem;
-    _Float16* const Kb1 = smem + TILE;
-    _Float16* const Vb0 = smem + 2 * TILE;
-    _Float16* const Vb1 = smem + 3 * TILE;
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int nqb = (S + 32 * NW - 1) / (32 * NW);
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = bid / nqb, qb = bid - bh * nqb;
-    const long base = (long)bh * S * D;
-    const int q = qb * 32 * NW + wave * 32 + r;
+__device__ __forceinline__ void fwd_init(FwdState<D>& st, const float* Q, long base, int q, int S, int h) {
     const float qscale = FA2_LOG2E / __builtin_sqrtf((float)D);
-
-    FwdState<D> st;
-#pragma unroll
-    for (int t = 0; t < D / 16; ++t) {
-        if (q < S) {
-            const f32x4* p = reinterpret_cast<const f32x4*>(Q + base + (long)q * D + 16 * t + 8 * h);
-            st.qf[t] = to_f16x8(p[0], p[1], qscale);
-        } else {
-            st.qf[t] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) st.oacc[b][i] = 0.f;
-    st.m = -__builtin_inff();
-    st.l = 0.f;
-
-    FragOffsets<D> fo;
-    fo.init(lane);
-    TileStager<D, KT, NT> ks, vs;
-    ks.init(K + base, S, tid);
-    vs.init(V + base, S, tid);
-    const int nt = (S + KT - 1) / KT;
-    const int last_ragged = (S % KT) ? nt - 1 : -1;
-
-    // prologue: K0, V0 -> LDS; S_0; K1 -> LDS
-    ks.load(0);
-    vs.load(0);
-    ks.store(Kb0, 1.f, tid);
-    vs.store(Vb0, 1.f, tid);
-    if (nt > 1) ks.load(KT);
-    __syncthreads();
-    f32x16 sA[2], sB[2];
-    fwd_qk<D>(sA, st, Kb0, fo);
-    if (nt > 1) ks.store(Kb1, 1.f, tid);
-    __syncthreads();
-
-    for (int j = 0; j < nt; j += 2) {
-        {  // step j: S_j in sA, K_{j+1} in Kb1, V_j in Vb0
-            const bool hn = j + 1 < nt, hnn = j + 2 < nt;
-            if (hn) vs.load((j + 1) * KT);
-            if (hnn) ks.load((j + 2) * KT);
-            if (hn) fwd_qk<D>(sB, st, Kb1, fo);
-            if (j == last_ragged) fwd_softmax_pv<D, true>(st, sA, Vb0, fo, j * KT, S, h);
-            else fwd_softmax_pv<D, false>(st, sA, Vb0, fo, j * KT, S, h);
-            if (hn) vs.store(Vb1, 1.f, tid);
-            if (hnn) ks.store(Kb0, 1.f, tid);
-            __syncthreads();
-        }
-        if (j + 1 < nt) {  // step j+1: S in sB, K_{j+2} in Kb0, V_{j+1} in Vb1
-            const bool hn = j + 2 < nt, hnn = j + 3 < nt;
-            if (hn) vs.load((j + 2) * KT);
-            if (hnn) ks.load((j + 3) * KT);
-            if (hn) fwd_qk<D>(sA, st, Kb0, fo);
-            if (j + 1 == last_ragged) fwd_softmax_pv<D, true>(st, sB, Vb1, fo, (j + 1) * KT, S, h);
-            else fwd_softmax_pv<D, false>(st, sB, Vb1, fo, (j + 1) * KT, S, h);
-            if (hn) vs.store(Vb0, 1.f, tid);
-            if (hnn) ks.store(Kb1, 1.f, tid);
-            __syncthreads();
-        }
-    }
-
-    const float lt = xor32_sum(st.l);
-    const float inv = 1.f / lt;
-    if (q < S) {
-        float* orow = O + base + (long)q * D;
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                f32x4 v = {st.oacc[b][4 * g] * inv, st.oacc[b][4 * g + 1] * inv, st.oacc[b][4 * g + 2] * inv,
-                           st.oacc[b][4 * g + 3] * inv};
-                *reinterpret_cast<f32x4*>(orow + 32 * b + 8 * g + 4 * h) = v;
-            }
-        if (h == 0) LSE[(long)bh * S + q] = st.m * FA2_LN2 + __logf(lt);
-    }
-}
-
-// Grid: BH * ceil(S / (32*NW)) workgroups of 64*NW threads (NW waves x 32 queries).
-template <int D, int NW>
-__global__ void __launch_bounds__(64 * NW)
-fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                   float* __restrict__ O, float* __restrict__ LSE, int S) {
-    constexpr int KT = 64;  // keys per tile
-    constexpr int NT = 64 * NW;
-    constexpr int TILE = KT * D;
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];  // [buf][K | V]
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int nqb = (S + 32 * NW - 1) / (32 * NW);
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = bid / nqb, qb = bid - bh * nqb;
-    const long base = (long)bh * S * D;
-    const int q = qb * 32 * NW + wave * 32 + r;
-    const float qscale = FA2_LOG2E / __builtin_sqrtf((float)D);
-
-    FwdState<D> st;
     // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16t + 8h + 0..7]
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
@@ -447,55 +337,17 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
         for (int i = 0; i < 16; ++i) st.oacc[b][i] = 0.f;
-    st.m = -__builtin_inff();
-    st.l = 0.f;
+    st.nm = splat16(0.f);
+    st.m = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) st.l[c] = 0.f;
+    st.pend = 0.f;
+}
 
-    FragOffsets<D> fo;
-    fo.init(lane);
-    TileStager<D, KT, NT> ks, vs;
-    ks.init(K + base, S, tid);
-    vs.init(V + base, S, tid);
-    const int ntiles = (S + KT - 1) / KT;
-    const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
-    ks.load(0);
-    vs.load(0);
-    ks.store(smem, 1.f, tid);
-    vs.store(smem + TILE, 1.f, tid);
-    __syncthreads();
-
-    // two tiles per trip so every LDS buffer offset is a compile-time immediate
-    for (int j = 0; j < ntiles; j += 2) {
-        {
-            const bool more = j + 1 < ntiles;
-            if (more) {
-                ks.load((j + 1) * KT);
-                vs.load((j + 1) * KT);
-            }
-            if (j == last_ragged) fwd_tile<D, true>(st, smem, smem + TILE, fo, j * KT, S, h);
-            else fwd_tile<D, false>(st, smem, smem + TILE, fo, j * KT, S, h);
-            if (more) {
-                ks.store(smem + 2 * TILE, 1.f, tid);
-                vs.store(smem + 3 * TILE, 1.f, tid);
-            }
-            __syncthreads();
-        }
-        if (j + 1 < ntiles) {
-            const bool more = j + 2 < ntiles;
-            if (more) {
-                ks.load((j + 2) * KT);
-                vs.load((j + 2) * KT);
-            }
-            if (j + 1 == last_ragged) fwd_tile<D, true>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
-            else fwd_tile<D, false>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
-            if (more) {
-                ks.store(smem, 1.f, tid);
-                vs.store(smem + TILE, 1.f, tid);
-            }
-            __syncthreads();
-        }
-    }
-
-    const float lt = xor32_sum(st.l);
+template <int D>
+__device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float* LSE, long base, long lrow, int q,
+                                          int S, int h) {
+    const float lt = xor32_sum((st.l[0] + st.l[1]) + (st.l[2] + st.l[3]));
     const float inv = 1.f / lt;
     if (q < S) {
         float* orow = O + base + (long)q * D;
@@ -507,8 +359,83 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                            st.oacc[b][4 * g + 3] * inv};
                 *reinterpret_cast<f32x4*>(orow + 32 * b + 8 * g + 4 * h) = v;
             }
-        if (h == 0) LSE[(long)bh * S + q] = st.m * FA2_LN2 + __logf(lt);
+        if (h == 0) LSE[lrow + q] = st.m * FA2_LN2 + __logf(lt);
     }
+}
+
+// Grid: BH * ceil(S / (32*NW)) workgroups of 64*NW threads (NW waves x 32 queries).
+// (A persistent variant that walks several query blocks per workgroup, with the
+// next block's Q prefetched by LDS-DMA and K/V streamed across block seams, cut
+// the per-block fixed cost from ~20 to ~16 us at C3 but ran the tile loop ~8 %
+// slower back-to-back, a net loss on the bench step -- r01)
+//
+// ABL: timing ablations only (tools/kbench.py, -DFA2_ABLATIONS builds; results
+// are wrong when set): 1 no staging in the loop, 2 no exp, 4 no barrier, 8 no PV
+// MFMAs, 16 no QK^T MFMAs, 32 no row max, 64 one KV tile only.
+template <int D, int NW, int ABL = 0>
+__global__ void __launch_bounds__(64 * NW)
+fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                   float* __restrict__ O, float* __restrict__ LSE, int S) {
+    constexpr int KT = 64;  // keys per tile
+    constexpr int NT = 64 * NW;
+    constexpr int TILE = KT * D;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];  // [buf][K | V]
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int nqb = (S + 32 * NW - 1) / (32 * NW);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = bid / nqb, qb = bid - bh * nqb;
+    const long base = (long)bh * S * D;
+    const int q = qb * 32 * NW + wave * 32 + r;
+
+    FwdState<D> st;
+    fwd_init<D>(st, Q, base, q, S, h);
+    FragOffsets<D> fo;
+    fo.init(lane);
+    TileStager<D, KT, NT> ks, vs;
+    ks.init(K + base, S, tid);
+    vs.init(V + base, S, tid);
+    const int ntiles = (ABL & 64) ? 1 : (S + KT - 1) / KT;
+    const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
+    ks.load(0);
+    vs.load(0);
+    ks.store(smem, 1.f, tid);
+    vs.store(smem + TILE, 1.f, tid);
+    __syncthreads();
+
+    // two tiles per trip so every LDS buffer offset is a compile-time immediate
+    for (int j = 0; j < ntiles; j += 2) {
+        {
+            const bool more = !(ABL & 1) && j + 1 < ntiles;
+            if (more) {
+                ks.load((j + 1) * KT);
+                vs.load((j + 1) * KT);
+            }
+            if (j == last_ragged) fwd_tile<D, true, ABL>(st, smem, smem + TILE, fo, j * KT, S, h, j == 0);
+            else fwd_tile<D, false, ABL>(st, smem, smem + TILE, fo, j * KT, S, h, j == 0);
+            if (more) {
+                ks.store(smem + 2 * TILE, 1.f, tid);
+                vs.store(smem + 3 * TILE, 1.f, tid);
+            }
+            if (!(ABL & 4)) __syncthreads();
+        }
+        if (j + 1 < ntiles) {
+            const bool more = !(ABL & 1) && j + 2 < ntiles;
+            if (more) {
+                ks.load((j + 2) * KT);
+                vs.load((j + 2) * KT);
+            }
+            if (j + 1 == last_ragged)
+                fwd_tile<D, true, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+            else fwd_tile<D, false, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+            if (more) {
+                ks.store(smem, 1.f, tid);
+                vs.store(smem + TILE, 1.f, tid);
+            }
+            if (!(ABL & 4)) __syncthreads();
+        }
+    }
+    fwd_store<D>(st, O, LSE, base, (long)bh * S, q, S, h);
 }
 
 }  // namespace fa2f16
@@ -516,26 +443,41 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
 #ifndef CUPY_INLINE_COMPILE
 namespace fa2 {
 
+template <int D, int NW, int ABL>
+static void fwd_f16_go(const float* q, const float* k, const float* v, float* o, float* lse, long grid, int S,
+                       hipStream_t stream) {
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
+                       v, o, lse, S);
+}
+
 template <int D, int NW>
 static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
                                  hipStream_t stream) {
     const int nqb = (S + 32 * NW - 1) / (32 * NW);
     const long grid = (long)bh * nqb;
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    if (tune_knob("FWD_PIPE", D <= 64 ? 1 : 0))
-        hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_pipe_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream,
-                           q, k, v, o, lse, S);
-    else
-        hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
-                           v, o, lse, S);
+#ifdef FA2_ABLATIONS
+    switch (tune_knob("FWD_ABL", 0)) {
+#define FA2_FWD_ABL(X) \
+    case X: fwd_f16_go<D, NW, X>(q, k, v, o, lse, grid, S, stream); return hipGetLastError();
+        FA2_FWD_ABL(1) FA2_FWD_ABL(2) FA2_FWD_ABL(4) FA2_FWD_ABL(8) FA2_FWD_ABL(16) FA2_FWD_ABL(24) FA2_FWD_ABL(32)
+        FA2_FWD_ABL(63) FA2_FWD_ABL(64)
+#undef FA2_FWD_ABL
+        default: break;
+    }
+#endif
+    fwd_f16_go<D, NW, 0>(q, k, v, o, lse, grid, S, stream);
     return hipGetLastError();
 }
 
 template <int D>
 static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
                                    hipStream_t stream) {
-    const int nw = tune_knob("FWD_WAVES", D <= 64 ? 8 : 4);
-    if (nw == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
+    // 8 waves (2 per SIMD) where the registers allow it; D = 128 runs 4 waves of
+    // ~400 VGPRs (8 would spill and exceed the LDS budget with the Q stages)
+    if constexpr (D <= 64) {
+        if (tune_knob("FWD_WAVES", 8) == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
+    }
     return fwd_f16_launch<D, 4>(q, k, v, o, lse, bh, S, stream);
 }
 

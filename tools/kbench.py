@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "cuda-flash-attention_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="4,16,2048,64")
-    ap.add_argument("--kernel", action="append", default=None, help="fwd|dkdv|dq|delta|bwd (repeatable)")
+    ap.add_argument("--kernel", action="append", default=None, help="fwd|dkdv|dq|delta|bwd|step (repeatable)")
     ap.add_argument("--variant", action="append", default=[], help="KNOB=V[,KNOB=V] (repeatable)")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
@@ -35,13 +35,17 @@ def main():
     o, lse = fa2amd.forward(q, k, v, "fp16")
     dl = fa2amd.delta(do, o)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
-    flops = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "delta": 0.0, "bwd": 10.0}
+    flops = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "delta": 0.0, "bwd": 10.0, "step": 14.0}
     calls = {
         "fwd": lambda: fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
         "dkdv": lambda: fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv),
         "dq": lambda: fa2amd.backward_dq(q, k, v, do, lse, dl, dq),
         "delta": lambda: fa2amd.delta(do, o, out=dl),
         "bwd": lambda: fa2amd.backward(q, k, v, o, do, lse, "fp16", dq=dq, dk=dk, dv=dv, delta_buf=dl),
+        # one bench.py step: fwd, delta, dK/dV, dQ in stream order
+        "step": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse), fa2amd.delta(do, o, out=dl),
+                         fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv),
+                         fa2amd.backward_dq(q, k, v, do, lse, dl, dq)),
     }
     kernels = args.kernel or ["fwd", "dkdv", "dq"]
     variants = args.variant or [""]
