@@ -72,8 +72,8 @@ class FA2Runner:
 
 class RawModuleRunner:
     """Drives kernels/kernel_fa2_optimized.cu and kernels/f-attn2-backward.cu exactly
-    as test_flash_attention2.py does through cp.RawModule (fp32 files only, like the
-    harness, :75-76)."""
+    as test_flash_attention2.py does through cp.RawModule (the harness names the fp32
+    files only, :75-76; the _f16 files export the same symbols and can be passed)."""
 
     BLOCK_SIZE_R = 32
     BLOCK_SIZE_C = 32

@@ -522,6 +522,185 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     }
 }
 
+// ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
+// block 256, test_flash_attention2.py:499-535 / f-attn2-backward_f16.cu:445),
+// fp16 tiles on MFMA.  A workgroup owns 32 keys (B operands K*log2e/sqrt(D) and
+// V in registers, K also as an LDS tile for dQ); its 32-row query tiles are dealt
+// to the 4 waves round-robin.  Per tile a wave stages Q into its private buffer
+// (S = Q K^T), then dO (dP = dO V^T, dV^T += dO^T P), then Q again (dK^T +=
+// Q^T dS); dS goes through a per-wave LDS scratch to become the A operand of
+// dQ += dS K / sqrt(D), which leaves as f32 atomics into the pre-zeroed dQ like
+// the reference's (f-attn2-backward_f16.cu:289).  The waves' dK / dV partials are
+// summed in a fixed order through one LDS buffer, so dK and dV are deterministic.
+struct CompatLds {
+    static constexpr int DMAX = 128;
+    static constexpr int SLD = 40;  // dS scratch row stride (halves): 80 B rows
+    static constexpr int BUF = 4 * 32 * DMAX;  // per-wave [32][D] tiles
+    static constexpr int KT = 32 * DMAX;       // this workgroup's K tile
+    static constexpr int DS = 4 * 32 * SLD;    // per-wave dS scratch [q][key]
+    static constexpr int HALVES = BUF + KT + DS;
+};
+
+template <int D>
+__device__ __forceinline__ void bwd_compat_body(const float* __restrict__ Q, const float* __restrict__ K,
+                                                const float* __restrict__ V, const float* __restrict__ dO,
+                                                const float* __restrict__ LSE, const float* __restrict__ Delta,
+                                                float* __restrict__ dQ, float* __restrict__ dK,
+                                                float* __restrict__ dV, int BH, int S, _Float16* lds,
+                                                float (*rowc)[2][32]) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int nkb = (S + 31) / 32;
+    const int bh = blockIdx.x / nkb, kb = blockIdx.x - bh * nkb;
+    if (bh >= BH) return;
+    const long base = (long)bh * S * D;
+    const long rbase = (long)bh * S;
+    const int k0 = kb * 32, key = k0 + r;
+    const bool kvalid = key < S;
+    const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
+    const float dscale = 1.f / __builtin_sqrtf((float)D);
+    _Float16* buf = lds + wave * 32 * D;
+    _Float16* Kt = lds + CompatLds::BUF;
+    _Float16* dsw = lds + CompatLds::BUF + CompatLds::KT + wave * 32 * CompatLds::SLD;
+
+    f16x8 kf[D / 16], vf[D / 16];
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+        kf[t] = load_frag(K + base + (long)key * D + 16 * t + 8 * h, kvalid, kscale);
+        vf[t] = load_frag(V + base + (long)key * D + 16 * t + 8 * h, kvalid, 1.f);
+    }
+    FragOffsets<D> fo;
+    fo.init(lane);
+    {
+        TileStager<D, 32, 256> kst;
+        kst.init(K + base, S, tid);
+        kst.load(k0);
+        kst.store(Kt, 1.f, tid);
+    }
+    __syncthreads();
+    f32x16 dka[D / 32], dva[D / 32];
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            dka[b][i] = 0.f;
+            dva[b][i] = 0.f;
+        }
+    TileStager<D, 32, 64> qs, ds;
+    qs.init(Q + base, S, lane);
+    ds.init(dO + base, S, lane);
+    const int nqt = (S + 31) / 32;
+    for (int j = wave; j < nqt; j += 4) {
+        const int q0 = j * 32;
+        if (h == 0) {
+            const int qi = q0 + r;
+            rowc[wave][0][r] = qi < S ? -LSE[rbase + qi] * FA2B_LOG2E : -__builtin_inff();
+            rowc[wave][1][r] = qi < S ? -Delta[rbase + qi] : 0.f;
+        }
+        qs.load(q0);
+        qs.store(buf, 1.f, lane);
+        f32x16 sa, da;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+            sa[i] = rowc[wave][0][row];
+            da[i] = rowc[wave][1][row];
+        }
+        // rows: query q0 + (i&3) + 8*(i>>2) + 4h ; col: key (lane)
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) sa = mfma(fo.rowop(buf, 0, t), kf[t], sa);
+        ds.load(q0);
+        ds.store(buf, 1.f, lane);
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) da = mfma(fo.rowop(buf, 0, t), vf[t], da);
+        f16x8 pf[2], dsf[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float p = kvalid ? fast_exp2(sa[i]) : 0.f;
+            const float dsv = p * da[i];
+            pf[i >> 3][i & 7] = (_Float16)p;
+            dsf[i >> 3][i & 7] = (_Float16)dsv;
+            dsw[((i & 3) + 8 * (i >> 2) + 4 * h) * CompatLds::SLD + r] = (_Float16)dsv;
+        }
+        // dV^T += dO^T P
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) dva[b] = mfma(fo.trop(buf, 16 * s, b), pf[s], dva[b]);
+        qs.store(buf, 1.f, lane);  // Q again (still in registers) for dK
+        // dK^T += Q^T dS
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) dka[b] = mfma(fo.trop(buf, 16 * s, b), dsf[s], dka[b]);
+        // dQ[q][d] += sum_key dS[q][key] K[key][d] / sqrt(D): A = dS rows (lane = query),
+        // B = K columns through the transposed read of the K tile
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b) {
+            f32x16 acc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                // k index (h, j) of trop's K rows is key 16s + 8(j>>2) + 4h + (j&3): read dS
+                // in that order, as two runs of four keys
+                const _Float16* d0 = dsw + r * CompatLds::SLD + 16 * s + 4 * h;
+                const i16x4 lo = *reinterpret_cast<const i16x4*>(d0);
+                const i16x4 hi = *reinterpret_cast<const i16x4*>(d0 + 8);
+                acc = mfma(cat4(lo, hi), fo.trop(Kt, 16 * s, b), acc);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int qi = q0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (qi < S) atomicAdd(dQ + base + (long)qi * D + 32 * b + r, acc[i] * dscale);
+            }
+        }
+    }
+    // sum the four waves' dK^T / dV^T in wave order through one [32][D] fp32 buffer
+    float* acc = reinterpret_cast<float*>(lds);
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int w = 0; w < 4; ++w) {
+            __syncthreads();
+            if (wave == w) {
+#pragma unroll
+                for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        float* a = acc + r * D + 32 * b + (i & 3) + 8 * (i >> 2) + 4 * h;
+                        const float v = pass == 0 ? dka[b][i] : dva[b][i];
+                        *a = w == 0 ? v : *a + v;
+                    }
+            }
+        }
+        __syncthreads();
+        float* dst = pass == 0 ? dK : dV;
+        const float sc = pass == 0 ? dscale : 1.f;
+        for (int x = tid; x < 32 * D; x += 256) {
+            const int row = x / D, d = x - row * D;
+            if (k0 + row < S) dst[base + (long)(k0 + row) * D + d] = acc[x] * sc;
+        }
+    }
+}
+
+// Δ = rowsum(dO ∘ O), one row per workgroup of any blockDim (the harness uses 64).
+__device__ __forceinline__ void delta_row_body(const float* __restrict__ dO, const float* __restrict__ O, long rows,
+                                               int D, float* __restrict__ Dvec) {
+    __shared__ float part[16];
+    const long row = blockIdx.x;
+    if (row >= rows) return;
+    float acc = 0.f;
+    for (int d = threadIdx.x; d < D; d += blockDim.x) acc += dO[row * D + d] * O[row * D + d];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    const int nw = (blockDim.x + 63) / 64;
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float s = 0.f;
+        for (int w = 0; w < nw; ++w) s += part[w];
+        Dvec[row] = s;
+    }
+}
+
 }  // namespace fa2f16b
 
 #ifndef CUPY_INLINE_COMPILE
@@ -650,4 +829,34 @@ void host_flash_attention2_backward_fp16(const float* h_Q, const float* h_K, con
 FA2_INST_BWD16(32)
 FA2_INST_BWD16(64)
 FA2_INST_BWD16(128)
+#else
+// CuPy face (same symbols as f-attn2-backward_f16.cu:477-514).  dQ, dK, dV arrive
+// zeroed (the harness's contract).  head_dim is honoured (32, 64, 128).  Static
+// LDS is ~51 KB, so the harness's dynamic bytes ((32D + 4*32D + 32 + 32*32)*4,
+// 45 184 at D = 64, 86 144 at D = 128) still fit in the 160 KiB of a workgroup.
+extern "C" __global__ void __launch_bounds__(256)
+flash_attention2_backward_kernel_wrapper(const float* query, const float* key, const float* value,
+                                         const float* output, const float* d_output, const float* logsumexp,
+                                         const float* d, float* d_query, float* d_key, float* d_value,
+                                         int batch_size, int num_heads, int seq_len, int head_dim) {
+    __shared__ __attribute__((aligned(16))) _Float16 lds[fa2f16b::CompatLds::HALVES];
+    __shared__ float rowc[4][2][32];
+    const int bh = batch_size * num_heads;
+    (void)output;
+    if (head_dim == 64)
+        fa2f16b::bwd_compat_body<64>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
+                                     lds, rowc);
+    else if (head_dim == 32)
+        fa2f16b::bwd_compat_body<32>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
+                                     lds, rowc);
+    else if (head_dim == 128)
+        fa2f16b::bwd_compat_body<128>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh,
+                                      seq_len, lds, rowc);
+}
+
+extern "C" __global__ void D_computation_reduction_kernel_wrapper(const float* d_output, const float* output,
+                                                                  int batch_size, int num_heads, int seq_len,
+                                                                  int head_dim, float* d) {
+    fa2f16b::delta_row_body(d_output, output, (long)batch_size * num_heads * seq_len, head_dim, d);
+}
 #endif  // CUPY_INLINE_COMPILE

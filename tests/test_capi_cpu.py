@@ -88,6 +88,8 @@ def test_cli_argv_contract(argv, needle):
 @pytest.mark.parametrize("fname,symbols", [
     ("kernel_fa2_optimized.cu", ["flash_attention2_forward_kernel_wrapper"]),
     ("f-attn2-backward.cu", ["D_computation_reduction_kernel_wrapper", "flash_attention2_backward_kernel_wrapper"]),
+    ("kernel_fa2_optimized_f16.cu", ["flash_attention2_forward_kernel_wrapper"]),
+    ("f-attn2-backward_f16.cu", ["D_computation_reduction_kernel_wrapper", "flash_attention2_backward_kernel_wrapper"]),
 ])
 def test_cupy_face_compiles_under_hiprtc(fname, symbols):
     """test_flash_attention2.py:113-145 compiles these files' text with
@@ -98,12 +100,15 @@ def test_cupy_face_compiles_under_hiprtc(fname, symbols):
         assert s in exported
 
 
+@pytest.mark.parametrize("suffix", ["", "_f16"])
 @pytest.mark.parametrize("D", [32, 64, 128])
-def test_cupy_face_lds_budget(D):
+def test_cupy_face_lds_budget(D, suffix):
     """static LDS + the harness's dynamic LDS (test_flash_attention2.py:278-281, 522-527)
     must fit the 160 KiB a workgroup may own, for every supported head_dim."""
-    fwd = rawmodule.static_lds_bytes(rawmodule.compile_source(rawmodule.load_kernel_source("kernel_fa2_optimized.cu")))
-    bwd = rawmodule.static_lds_bytes(rawmodule.compile_source(rawmodule.load_kernel_source("f-attn2-backward.cu")))
+    fwd = rawmodule.static_lds_bytes(rawmodule.compile_source(
+        rawmodule.load_kernel_source(f"kernel_fa2_optimized{suffix}.cu")))
+    bwd = rawmodule.static_lds_bytes(rawmodule.compile_source(
+        rawmodule.load_kernel_source(f"f-attn2-backward{suffix}.cu")))
     dyn_fwd = (32 * D * 2 + 32 * D + 32 * 32 + 32 * 3) * 4
     dyn_bwd = (32 * D + 32 * D * 4 + 32 + 32 * 32) * 4
     assert fwd["flash_attention2_forward_kernel_wrapper"] + dyn_fwd <= rawmodule.MAX_LDS_BYTES
