@@ -25,6 +25,10 @@
 // cp.RawModule path, test_flash_attention2.py:113-126), C++14 only.
 #ifndef CUPY_INLINE_COMPILE
 #include "f-attn2.cuh"
+#ifdef FA2_STAMPS
+#include <cstdio>
+#include <vector>
+#endif
 #endif
 
 namespace fa2f16 {
@@ -191,23 +195,26 @@ __device__ __forceinline__ float xor32_sum(float x) {
 // forward
 // ---------------------------------------------------------------------------
 // Online-softmax state of one wave: 32 query rows (one per lane pair), O^T
-// accumulator (d on the rows), running max m (log2 domain), per-half sum l, and
-// nm = -m broadcast over 16 registers: the initial value of every S^T
-// accumulator, so the QK^T MFMAs produce s - m directly (no per-score v_sub).
-// pend: shift not yet applied to an S^T tile that was issued before m last moved
-// (software pipelining; 0 almost always).
+// accumulator (d on the rows), running max m (log2 domain), four partial row sums
+// (four short dependency chains per tile, not one of 32), and nm = -m broadcast
+// over 16 registers: the initial value of every S^T accumulator, so the QK^T
+// MFMAs produce s - m directly (no per-score v_sub).
 template <int D>
 struct FwdState {
     f16x8 qf[D / 16];
     f32x16 oacc[D / 32];
     f32x16 nm;
-    float m, pend;
-    float l[4];  // four partial row sums: four short dependency chains per tile, not one of 32
+    float m;
+    float l[4];
 };
 
-// Lazy rescale (guide T13): the running max moves only when a tile's max
-// exceeds it by more than RESCALE_THR (log2 units), so p <= 2^8 in fp16/fp32.
-#define FA2_RESCALE_THR 8.0f
+// Lazy rescale (guide T13) without a per-tile row max: m is the row max of the
+// first tile and moves only when a tile's scores could overflow.  The common path
+// computes p = exp2(s - m) and the tile's row sum straight away; a half-row sum
+// above 2^13 (or inf / NaN) sends the whole wave to the slow path, which takes the
+// row max, moves m, rescales l and O and recomputes the tile.  Every p the common
+// path keeps is therefore <= 2^13: exact-range fp16 for the PV operand.
+#define FA2_TILE_SUM_MAX 8192.0f
 
 // -m as one opaque 16-register tuple: without the empty asm the compiler
 // rematerialises the splat with 16 v_mov before every QK^T chain.
@@ -247,21 +254,58 @@ __device__ __forceinline__ float tile_max(const f32x16 (&t)[2]) {
     return fmaxf(fmaxf(c[0], c[1]), fmaxf(c[2], c[3]));
 }
 
-// p = exp2(s - m - sh) (sh = 0 on the common path), row sum, O^T += V^T P^T with
-// the packed scores as the B operand.
-template <int D, bool SHIFT, int ABL = 0>
-__device__ __forceinline__ void fwd_exp_pv(FwdState<D>& st, const f32x16 (&sacc)[2], float sh, const _Float16* Vs,
-                                           const FragOffsets<D>& fo) {
-    f16x8 pf[2][2];
+// p = exp2(s - m - sh) of the tile, packed to fp16, with its four partial row sums.
+template <bool SHIFT, int ABL = 0>
+__device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[2], float sh, f16x8 (&pf)[2][2], float (&ls)[4]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ls[c] = 0.f;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const float x = SHIFT ? sacc[kb][i] - sh : sacc[kb][i];
             const float p = (ABL & 2) ? x : fast_exp2(x);
-            st.l[i & 3] += p;
+            ls[i & 3] += p;
             pf[kb][i >> 3][i & 7] = (_Float16)p;
         }
+}
+
+// Online softmax of one tile (sacc = s - m) and O^T += V^T P^T with the packed
+// scores as the B operand.  first: the wave's first tile (m := its row max).
+template <int D, bool MASK, int ABL = 0>
+__device__ __forceinline__ void fwd_softmax_pv(FwdState<D>& st, f32x16 (&sacc)[2], const _Float16* Vs,
+                                               const FragOffsets<D>& fo, int k0, int S, int h, bool first) {
+    if (MASK) {  // ragged last tile only
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[kb][i] = -__builtin_inff();
+    }
+    f16x8 pf[2][2];
+    float ls[4];
+    bool slow = first;
+    if (!first) {
+        fwd_exp<false, ABL>(sacc, 0.f, pf, ls);
+        const float ts = (ls[0] + ls[1]) + (ls[2] + ls[3]);
+        slow = !(ABL & 32) && __any(!(ts <= FA2_TILE_SUM_MAX));
+    }
+    if (slow) {
+        const float mx = xor32_max(tile_max(sacc));
+        const float d = first ? mx : fmaxf(mx, 0.f);
+        const float alpha = first ? 0.f : fast_exp2(-d);
+        st.m += d;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st.l[c] *= alpha;
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) st.oacc[b][i] *= alpha;
+        st.nm = splat16(-st.m);
+        fwd_exp<true, ABL>(sacc, d, pf, ls);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) st.l[c] += ls[c];
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
@@ -273,51 +317,13 @@ __device__ __forceinline__ void fwd_exp_pv(FwdState<D>& st, const f32x16 (&sacc)
             }
 }
 
-// Online softmax of one tile (sacc = s - m + pend).  The common path is exp + PV
-// only; when m moves (first tile: m := row max; later: a row max more than
-// RESCALE_THR above m) the slow path rescales l and O and shifts the scores.
-// NEXT: the next tile's scores were already issued against the old m, so they
-// carry the shift in pend.
-template <int D, bool MASK, bool NEXT, int ABL = 0>
-__device__ __forceinline__ void fwd_softmax_pv(FwdState<D>& st, f32x16 (&sacc)[2], const _Float16* Vs,
-                                               const FragOffsets<D>& fo, int k0, int S, int h, bool first) {
-    if (MASK) {  // ragged last tile only
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[kb][i] = -__builtin_inff();
-    }
-    float mx = tile_max(sacc);
-    mx = xor32_max(mx) - st.pend;
-    if (ABL & 32) mx = sacc[0][0];
-    const bool grow = first || mx > FA2_RESCALE_THR;
-    if (__any(grow || st.pend != 0.f)) {
-        const float d = grow ? mx : 0.f;
-        const float alpha = first ? 0.f : fast_exp2(-d);
-        const float sh = st.pend + d;
-        st.m += d;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) st.l[c] *= alpha;
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) st.oacc[b][i] *= alpha;
-        st.nm = splat16(-st.m);
-        st.pend = NEXT ? d : 0.f;
-        fwd_exp_pv<D, true, ABL>(st, sacc, sh, Vs, fo);
-    } else {
-        fwd_exp_pv<D, false, ABL>(st, sacc, 0.f, Vs, fo);
-    }
-}
-
-// One 64-key tile, unpipelined: QK^T, then softmax and PV.
+// One 64-key tile: QK^T, then softmax and PV.
 template <int D, bool MASK, int ABL = 0>
 __device__ __forceinline__ void fwd_tile(FwdState<D>& st, const _Float16* Ks, const _Float16* Vs,
                                          const FragOffsets<D>& fo, int k0, int S, int h, bool first) {
     f32x16 sacc[2];
     fwd_qk<D, ABL>(sacc, st, Ks, fo);
-    fwd_softmax_pv<D, MASK, false, ABL>(st, sacc, Vs, fo, k0, S, h, first);
+    fwd_softmax_pv<D, MASK, ABL>(st, sacc, Vs, fo, k0, S, h, first);
 }
 
 template <int D>
@@ -341,7 +347,6 @@ __device__ __forceinline__ void fwd_init(FwdState<D>& st, const float* Q, long b
     st.m = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) st.l[c] = 0.f;
-    st.pend = 0.f;
 }
 
 template <int D>
@@ -371,11 +376,31 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 //
 // ABL: timing ablations only (tools/kbench.py, -DFA2_ABLATIONS builds; results
 // are wrong when set): 1 no staging in the loop, 2 no exp, 4 no barrier, 8 no PV
-// MFMAs, 16 no QK^T MFMAs, 32 no row max, 64 one KV tile only.
+// MFMAs, 16 no QK^T MFMAs, 32 never take the slow path, 64 one KV tile only.
+// FA2_STAMPS (diagnostic builds only): s_memtime at the loop's segment boundaries,
+// per-wave sums written to `stamps` (read the shares, never the build's run time:
+// the stamps' fences forbid overlaps the real kernel has; guide §7 'In-kernel stamps').
+#ifdef FA2_STAMPS
+#define FA2_NSTAMP 5
+#define FA2_STAMP(k)                                                                              \
+    do {                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        unsigned long long t_;                                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        stv[k] += t_ - tprev;                                                                     \
+        tprev = t_;                                                                               \
+    } while (0)
+#define FA2_STAMP_ARG , unsigned long long* __restrict__ stamps
+#else
+#define FA2_STAMP(k)
+#define FA2_STAMP_ARG
+#endif
+
 template <int D, int NW, int ABL = 0>
 __global__ void __launch_bounds__(64 * NW)
 fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                   float* __restrict__ O, float* __restrict__ LSE, int S) {
+                   float* __restrict__ O, float* __restrict__ LSE, int S FA2_STAMP_ARG) {
     constexpr int KT = 64;  // keys per tile
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
@@ -403,6 +428,10 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     vs.store(smem + TILE, 1.f, tid);
     __syncthreads();
 
+#ifdef FA2_STAMPS
+    unsigned long long stv[FA2_NSTAMP] = {0, 0, 0, 0, 0}, tprev;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
+#endif
     // two tiles per trip so every LDS buffer offset is a compile-time immediate
     for (int j = 0; j < ntiles; j += 2) {
         {
@@ -411,13 +440,20 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                 ks.load((j + 1) * KT);
                 vs.load((j + 1) * KT);
             }
-            if (j == last_ragged) fwd_tile<D, true, ABL>(st, smem, smem + TILE, fo, j * KT, S, h, j == 0);
-            else fwd_tile<D, false, ABL>(st, smem, smem + TILE, fo, j * KT, S, h, j == 0);
+            FA2_STAMP(0);
+            f32x16 sacc[2];
+            fwd_qk<D, ABL>(sacc, st, smem, fo);
+            FA2_STAMP(1);
+            if (j == last_ragged) fwd_softmax_pv<D, true, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
+            else fwd_softmax_pv<D, false, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
+            FA2_STAMP(2);
             if (more) {
                 ks.store(smem + 2 * TILE, 1.f, tid);
                 vs.store(smem + 3 * TILE, 1.f, tid);
             }
+            FA2_STAMP(3);
             if (!(ABL & 4)) __syncthreads();
+            FA2_STAMP(4);
         }
         if (j + 1 < ntiles) {
             const bool more = !(ABL & 1) && j + 2 < ntiles;
@@ -425,16 +461,27 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                 ks.load((j + 2) * KT);
                 vs.load((j + 2) * KT);
             }
+            FA2_STAMP(0);
+            f32x16 sacc[2];
+            fwd_qk<D, ABL>(sacc, st, smem + 2 * TILE, fo);
+            FA2_STAMP(1);
             if (j + 1 == last_ragged)
-                fwd_tile<D, true, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
-            else fwd_tile<D, false, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+                fwd_softmax_pv<D, true, ABL>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+            else fwd_softmax_pv<D, false, ABL>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+            FA2_STAMP(2);
             if (more) {
                 ks.store(smem, 1.f, tid);
                 vs.store(smem + TILE, 1.f, tid);
             }
+            FA2_STAMP(3);
             if (!(ABL & 4)) __syncthreads();
+            FA2_STAMP(4);
         }
     }
+#ifdef FA2_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blockIdx.x * NW + wave) * FA2_NSTAMP + k] = stv[k];
+#endif
     fwd_store<D>(st, O, LSE, base, (long)bh * S, q, S, h);
 }
 
@@ -474,8 +521,8 @@ __device__ __forceinline__ void fwd_compat_body(const float* __restrict__ Q, con
         fwd_qk<D>(sacc, st, buf, fo);
         vs.load(j * KT);
         vs.store(buf, 1.f, lane);  // after this wave's K reads (in-order LDS within a wave)
-        if ((j + 1) * KT > S) fwd_softmax_pv<D, true, false>(st, sacc, buf, fo, j * KT, S, h, j == wave);
-        else fwd_softmax_pv<D, false, false>(st, sacc, buf, fo, j * KT, S, h, j == wave);
+        if ((j + 1) * KT > S) fwd_softmax_pv<D, true>(st, sacc, buf, fo, j * KT, S, h, j == wave);
+        else fwd_softmax_pv<D, false>(st, sacc, buf, fo, j * KT, S, h, j == wave);
     }
     // merge: O = sum_w 2^(m_w - M) O_w / sum_w 2^(m_w - M) l_w, M = max_w m_w
     const float lw = xor32_sum((st.l[0] + st.l[1]) + (st.l[2] + st.l[3]));
@@ -512,11 +559,46 @@ __device__ __forceinline__ void fwd_compat_body(const float* __restrict__ Q, con
 #ifndef CUPY_INLINE_COMPILE
 namespace fa2 {
 
+#ifdef FA2_STAMPS
+// diagnostic: accumulate the per-wave segment sums of every launch, print shares at exit
+struct StampLog {
+    double sum[FA2_NSTAMP] = {};
+    long launches = 0;
+    ~StampLog() {
+        double t = 0;
+        for (double x : sum) t += x;
+        if (!launches || t <= 0) return;
+        const char* names[FA2_NSTAMP] = {"load-issue", "qk", "softmax+pv", "lds-store", "barrier"};
+        fprintf(stderr, "[fa2 stamps] fwd launches=%ld cycles/wave/launch=%.0f\n", launches, t / launches);
+        for (int k = 0; k < FA2_NSTAMP; ++k) fprintf(stderr, "[fa2 stamps]   %-12s %5.1f %%\n", names[k], 100 * sum[k] / t);
+    }
+};
+static StampLog g_stamps;
+#endif
+
 template <int D, int NW, int ABL>
 static void fwd_f16_go(const float* q, const float* k, const float* v, float* o, float* lse, long grid, int S,
                        hipStream_t stream) {
+#ifdef FA2_STAMPS
+    static unsigned long long* buf = nullptr;
+    static long cap = 0;
+    const long n = grid * NW * FA2_NSTAMP;
+    if (n > cap) {
+        if (buf) (void)hipFree(buf);
+        (void)hipMalloc(&buf, n * sizeof(unsigned long long));
+        cap = n;
+    }
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
+                       v, o, lse, S, buf);
+    std::vector<unsigned long long> h(n);
+    (void)hipStreamSynchronize(stream);
+    (void)hipMemcpy(h.data(), buf, n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    for (long i = 0; i < n; ++i) g_stamps.sum[i % FA2_NSTAMP] += (double)h[i] / (grid * NW);
+    ++g_stamps.launches;
+#else
     hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
                        v, o, lse, S);
+#endif
 }
 
 template <int D, int NW>
