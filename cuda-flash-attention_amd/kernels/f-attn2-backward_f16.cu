@@ -26,6 +26,10 @@
 // Self-contained device code (hiprtc-compilable with -DCUPY_INLINE_COMPILE, C++14).
 #ifndef CUPY_INLINE_COMPILE
 #include "f-attn2.cuh"
+#ifdef FA2_STAMPS
+#include <cstdio>
+#include <vector>
+#endif
 #endif
 
 namespace fa2f16b {
@@ -186,11 +190,13 @@ struct DkdvState {
 // B operands.  Every LDS fragment (Q / dO rows, dO^T / Q^T columns) feeds KB MFMAs.
 // ABL (timing ablations only, tools/kbench.py; results are wrong when set):
 //   2 = no softmax VALU, 8 = no dV/dK MFMAs, 16 = no S/dP MFMAs
-template <int D, int KB, int ABL = 0>
+template <int D, int KB, int ABL = 0, typename Mid>
 __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* Qs, const _Float16* dOs,
-                                          const float* nlse2, const float* ndel, const FragOffsets<D>& fo, int h) {
+                                          const float* nlse2, const float* ndel, const FragOffsets<D>& fo, int h,
+                                          Mid&& mid) {
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
+        if (qb == 1) mid();  // between the two query blocks (staging loads, FA2_DKDV_LP)
         // accumulator rows: query qb*32 + (i&3) + 8*(i>>2) + 4h ; col: key (lane)
         f32x16 init_s, init_d;
 #pragma unroll
@@ -256,13 +262,40 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
     }
 }
 
+#ifndef FA2_DKDV_LP
+#define FA2_DKDV_LP 1
+#endif
+#ifndef FA2_DQ_LP
+#define FA2_DQ_LP 1
+#endif
+
+// FA2_STAMPS (diagnostic builds only): s_memtime at the loop's segment boundaries,
+// per-wave sums written to `stamps` (read the shares, never the build's run time).
+#ifdef FA2_STAMPS
+#define FA2_NSTAMP 5
+#define FA2_STAMP(k)                                                                              \
+    do {                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        unsigned long long t_;                                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        stv[k] += t_ - tprev;                                                                     \
+        tprev = t_;                                                                               \
+    } while (0)
+#define FA2_STAMP_ARG , unsigned long long* __restrict__ stamps
+#else
+#define FA2_STAMP(k)
+#define FA2_STAMP_ARG
+#endif
+
 // KB x 32 keys per wave, NW waves: grid BH * ceil(S / (32*KB*NW)), block 64*NW.
 // ABL: timing ablations (see dkdv_step; plus 1 = no staging in the loop, 4 = no barrier)
 template <int D, int NW, int KB = 1, int ABL = 0>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                         const float* __restrict__ dO, const float* __restrict__ LSE,
-                        const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV, int S) {
+                        const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV,
+                        int S FA2_STAMP_ARG) {
     constexpr int QT = 64;  // query rows per step
     constexpr int NT = 64 * NW;
     constexpr int TILE = QT * D;
@@ -324,43 +357,77 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
         if (wave_u == 0) rows[buf][0][lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
         else if (wave_u == 1) rows[buf][1][lane] = -rowraw;
     };
-    auto load_step = [&](int it) {
-        qs.load(it * QT);
-        dos.load(it * QT);
-        load_rows(it * QT);
+    // where the next step's global loads are issued (all eight waves issuing them at
+    // once right after the barrier queue on the texture unit): FA2_DKDV_LP
+    // 0 = all at the step start, 1 = all between the two query blocks, 2 = Q at the
+    // start and dO + row constants between the blocks
+    auto load_a = [&](int it) {
+        if (FA2_DKDV_LP == 0 || FA2_DKDV_LP == 2) qs.load(it * QT);
+        if (FA2_DKDV_LP == 0) {
+            dos.load(it * QT);
+            load_rows(it * QT);
+        }
     };
-
+    auto load_b = [&](int it) {
+        if (FA2_DKDV_LP == 1) qs.load(it * QT);
+        if (FA2_DKDV_LP != 0) {
+            dos.load(it * QT);
+            load_rows(it * QT);
+        }
+    };
     const int nsteps = (S + QT - 1) / QT;
-    load_step(0);
+    qs.load(0);
+    dos.load(0);
+    load_rows(0);
     qs.store(smem, 1.f, tid);
     dos.store(smem + TILE, 1.f, tid);
     store_rows(0);
     __syncthreads();
 
+#ifdef FA2_STAMPS
+    unsigned long long stv[FA2_NSTAMP] = {0, 0, 0, 0, 0}, tprev;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
+#endif
     for (int it = 0; it < nsteps; it += 2) {
         {
             const bool more = !(ABL & 1) && it + 1 < nsteps;
-            if (more) load_step(it + 1);
-            dkdv_step<D, KB, ABL>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h);
+            if (more) load_a(it + 1);
+            FA2_STAMP(0);
+            dkdv_step<D, KB, ABL>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h, [&] {
+                if (more) load_b(it + 1);
+            });
+            FA2_STAMP(1);
             if (more) {
                 qs.store(smem + 2 * TILE, 1.f, tid);
                 dos.store(smem + 3 * TILE, 1.f, tid);
                 store_rows(1);
             }
+            FA2_STAMP(2);
             if (!(ABL & 4)) __syncthreads();
+            FA2_STAMP(3);
         }
         if (it + 1 < nsteps) {
             const bool more = !(ABL & 1) && it + 2 < nsteps;
-            if (more) load_step(it + 2);
-            dkdv_step<D, KB, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h);
+            if (more) load_a(it + 2);
+            FA2_STAMP(0);
+            dkdv_step<D, KB, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h, [&] {
+                if (more) load_b(it + 2);
+            });
+            FA2_STAMP(1);
             if (more) {
                 qs.store(smem, 1.f, tid);
                 dos.store(smem + TILE, 1.f, tid);
                 store_rows(0);
             }
+            FA2_STAMP(2);
             if (!(ABL & 4)) __syncthreads();
+            FA2_STAMP(3);
         }
     }
+#ifdef FA2_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blockIdx.x * NW + wave) * FA2_NSTAMP + k] = stv[k];
+#endif
 
     const float dscale = 1.f / __builtin_sqrtf((float)D);
 #pragma unroll
@@ -396,12 +463,13 @@ struct DqState {
 
 // One 64-key tile: S^T = K Q^T and dP^T = V dO^T with the query on the lane,
 // dS^T = P^T*(dP^T - Delta), dQ^T += K^T dS^T (K^T through ds_read_b64_tr_b16).
-template <int D, bool MASK>
+template <int D, bool MASK, typename Mid>
 __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, const _Float16* Vs,
-                                        const FragOffsets<D>& fo, int k0, int S, int h) {
+                                        const FragOffsets<D>& fo, int k0, int S, int h, Mid&& mid) {
     f16x8 dsf[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+        if (kb == 1) mid();  // between the two key blocks (next tile's loads, FA2_DQ_LP)
         // rows: key k0 + kb*32 + (i&3) + 8*(i>>2) + 4h ; col: query (lane)
         f32x16 sa = st.nlse2, da = st.ndel;
 #pragma unroll
@@ -480,12 +548,16 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     for (int j = 0; j < ntiles; j += 2) {
         {
             const bool more = j + 1 < ntiles;
-            if (more) {
+            auto ld = [&] {
                 ks.load((j + 1) * KT);
                 vs.load((j + 1) * KT);
-            }
-            if (j == last_ragged) dq_tile<D, true>(st, smem, smem + TILE, fo, j * KT, S, h);
-            else dq_tile<D, false>(st, smem, smem + TILE, fo, j * KT, S, h);
+            };
+            if (more && !FA2_DQ_LP) ld();
+            auto mid = [&] {
+                if (more && FA2_DQ_LP) ld();
+            };
+            if (j == last_ragged) dq_tile<D, true>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
+            else dq_tile<D, false>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
             if (more) {
                 ks.store(smem + 2 * TILE, 1.f, tid);
                 vs.store(smem + 3 * TILE, 1.f, tid);
@@ -494,12 +566,17 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
         }
         if (j + 1 < ntiles) {
             const bool more = j + 2 < ntiles;
-            if (more) {
+            auto ld = [&] {
                 ks.load((j + 2) * KT);
                 vs.load((j + 2) * KT);
-            }
-            if (j + 1 == last_ragged) dq_tile<D, true>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
-            else dq_tile<D, false>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h);
+            };
+            if (more && !FA2_DQ_LP) ld();
+            auto mid = [&] {
+                if (more && FA2_DQ_LP) ld();
+            };
+            if (j + 1 == last_ragged)
+                dq_tile<D, true>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
+            else dq_tile<D, false>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
             if (more) {
                 ks.store(smem, 1.f, tid);
                 vs.store(smem + TILE, 1.f, tid);
@@ -707,6 +784,21 @@ __device__ __forceinline__ void delta_row_body(const float* __restrict__ dO, con
 namespace fa2 {
 
 namespace {
+#ifdef FA2_STAMPS
+struct StampLog {
+    double sum[FA2_NSTAMP] = {};
+    long launches = 0;
+    ~StampLog() {
+        double t = 0;
+        for (double x : sum) t += x;
+        if (!launches || t <= 0) return;
+        const char* names[FA2_NSTAMP] = {"load-issue", "step", "lds-store", "barrier", "-"};
+        fprintf(stderr, "[fa2 stamps] dkdv launches=%ld cycles/wave/launch=%.0f\n", launches, t / launches);
+        for (int k = 0; k < 4; ++k) fprintf(stderr, "[fa2 stamps]   %-12s %5.1f %%\n", names[k], 100 * sum[k] / t);
+    }
+};
+StampLog g_dkdv_stamps;
+#endif
 // waves per workgroup: 8 x 32 keys for D <= 64 (2 waves/SIMD fit in 256 VGPRs);
 // D = 128 needs more than 256 registers per lane, so 4 waves (1 per SIMD).
 template <int D, int NW, int KB = 1, int ABL = 0>
@@ -714,8 +806,26 @@ hipError_t dkdv_launch(const float* q, const float* k, const float* v, const flo
                        const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
     const long grid = (long)bh * ((S + 32 * KB * NW - 1) / (32 * KB * NW));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+#ifdef FA2_STAMPS
+    static unsigned long long* buf = nullptr;
+    static long cap = 0;
+    const long n = grid * NW * FA2_NSTAMP;
+    if (n > cap) {
+        if (buf) (void)hipFree(buf);
+        (void)hipMalloc(&buf, n * sizeof(unsigned long long));
+        cap = n;
+    }
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, KB, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0,
+                       stream, q, k, v, dout, lse, delta, dk, dv, S, buf);
+    std::vector<unsigned long long> hst(n);
+    (void)hipStreamSynchronize(stream);
+    (void)hipMemcpy(hst.data(), buf, n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    for (long i = 0; i < n; ++i) g_dkdv_stamps.sum[i % FA2_NSTAMP] += (double)hst[i] / (grid * NW);
+    ++g_dkdv_stamps.launches;
+#else
     hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, KB, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0,
                        stream, q, k, v, dout, lse, delta, dk, dv, S);
+#endif
     return hipGetLastError();
 }
 // Geometry (FA2_TUNE_DKDV_WAVES / FA2_TUNE_DKDV_KB): 8 waves x 32 keys for D <= 64

@@ -377,6 +377,13 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 // ABL: timing ablations only (tools/kbench.py, -DFA2_ABLATIONS builds; results
 // are wrong when set): 1 no staging in the loop, 2 no exp, 4 no barrier, 8 no PV
 // MFMAs, 16 no QK^T MFMAs, 32 never take the slow path, 64 one KV tile only.
+// FA2_FWD_LP: 0 = the next tile's global loads at the tile start, 1 = after QK^T
+// (guide T14: the eight waves' loads then queue on the texture unit under the
+// softmax instead of stalling every wave at the tile start)
+#ifndef FA2_FWD_LP
+#define FA2_FWD_LP 1
+#endif
+
 // FA2_STAMPS (diagnostic builds only): s_memtime at the loop's segment boundaries,
 // per-wave sums written to `stamps` (read the shares, never the build's run time:
 // the stamps' fences forbid overlaps the real kernel has; guide §7 'In-kernel stamps').
@@ -436,13 +443,17 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     for (int j = 0; j < ntiles; j += 2) {
         {
             const bool more = !(ABL & 1) && j + 1 < ntiles;
-            if (more) {
+            if (more && !FA2_FWD_LP) {
                 ks.load((j + 1) * KT);
                 vs.load((j + 1) * KT);
             }
             FA2_STAMP(0);
             f32x16 sacc[2];
             fwd_qk<D, ABL>(sacc, st, smem, fo);
+            if (more && FA2_FWD_LP) {
+                ks.load((j + 1) * KT);
+                vs.load((j + 1) * KT);
+            }
             FA2_STAMP(1);
             if (j == last_ragged) fwd_softmax_pv<D, true, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
             else fwd_softmax_pv<D, false, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
@@ -457,13 +468,17 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         }
         if (j + 1 < ntiles) {
             const bool more = !(ABL & 1) && j + 2 < ntiles;
-            if (more) {
+            if (more && !FA2_FWD_LP) {
                 ks.load((j + 2) * KT);
                 vs.load((j + 2) * KT);
             }
             FA2_STAMP(0);
             f32x16 sacc[2];
             fwd_qk<D, ABL>(sacc, st, smem + 2 * TILE, fo);
+            if (more && FA2_FWD_LP) {
+                ks.load((j + 2) * KT);
+                vs.load((j + 2) * KT);
+            }
             FA2_STAMP(1);
             if (j + 1 == last_ragged)
                 fwd_softmax_pv<D, true, ABL>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
