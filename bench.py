@@ -95,6 +95,70 @@ def cpu_baseline(S, D, sample_heads=None):
             "sample": f"{heads} heads x (S={S}, D={D}) fp32 fwd+bwd, oracle/fa2_oracle.c, {dt:.2f} s"}
 
 
+def time_config(fa2amd, torch, dev, B, H, S, D, prec, fwd_only, iters=10, warmup=3):
+    """Mean ms of fwd (+ bwd) on one synthetic config (harness distribution), events on
+    the current stream; returns (ms, tflops, gbps) with the algorithmic counts."""
+    gen = torch.Generator().manual_seed(7)
+    q, k, v = (torch.rand(B, H, S, D, generator=gen).to(dev) for _ in range(3))
+    do = torch.ones_like(q)
+    o, lse = torch.empty_like(q), torch.empty(B, H, S, device=dev)
+    dq, dk, dv, dl = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q), torch.empty(B, H, S, device=dev)
+
+    def once():
+        fa2amd.forward(q, k, v, prec, out=o, lse=lse)
+        if not fwd_only:
+            fa2amd.backward(q, k, v, o, do, lse, prec, dq=dq, dk=dk, dv=dv, delta_buf=dl)
+
+    for _ in range(warmup):
+        once()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    e0.record()
+    for _ in range(iters):
+        once()
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = (4.0 if fwd_only else 14.0) * B * H * S * S * D
+    nbytes = (16.0 * S * D + 4.0 * S if fwd_only else 48.0 * S * D + 8.0 * S) * B * H
+    return ms, flops / ms / 1e9, nbytes / ms / 1e6
+
+
+def torch_sdpa_cpu(S, D, heads):
+    """PyTorch-CPU SDPA fwd+bwd (autograd) on the host cores: the reference harness's
+    CPU baseline (test_flash_attention2.py), timed beside the oracle port."""
+    import torch
+
+    threads = max(1, min(len(os.sched_getaffinity(0)), 16))
+    torch.set_num_threads(threads)
+    gen = torch.Generator().manual_seed(42)
+    q, k, v = (torch.rand(1, heads, S, D, generator=gen).requires_grad_() for _ in range(3))
+    t0 = time.perf_counter()
+    o = torch.nn.functional.scaled_dot_product_attention(q, k, v)
+    o.backward(torch.ones_like(o))
+    dt = time.perf_counter() - t0
+    return {"value": round(14.0 * heads * S * S * D / dt / 1e12, 5), "unit": "TFLOPS", "cores": threads,
+            "sample": f"{heads} heads x (S={S}, D={D}) fp32 torch SDPA fwd+bwd (autograd), {dt:.2f} s"}
+
+
+def extras(fa2amd, torch, dev):
+    """north_star's sweep and BASELINE.json's other GPU configs, each against its roofline."""
+    out = {"sweep_B2_H8_D64_fp16_fwdbwd": {}}
+    for S in (512, 1024, 2048, 4096):
+        ms, tf, gbps = time_config(fa2amd, torch, dev, 2, 8, S, 64, "fp16", False)
+        out["sweep_B2_H8_D64_fp16_fwdbwd"][str(S)] = {"ms": round(ms, 4), "tflops": round(tf, 2),
+                                                      "hbm_gbps": round(gbps, 1),
+                                                      "frac_mfma": round(tf / MFMA_F16_PEAK_TFLOPS, 4)}
+    ms, tf, gbps = time_config(fa2amd, torch, dev, 8, 16, 4096, 128, "fp16", True, iters=5)
+    out["c4_B8_H16_S4096_D128_fp16_fwd"] = {"ms": round(ms, 4), "tflops": round(tf, 2), "hbm_gbps": round(gbps, 1),
+                                            "frac_mfma": round(tf / MFMA_F16_PEAK_TFLOPS, 4),
+                                            "frac_hbm": round(gbps / HBM_PEAK_GBPS, 4)}
+    ms, tf, gbps = time_config(fa2amd, torch, dev, 2, 8, 512, 64, "fp32", False)
+    out["c2_B2_H8_S512_D64_fp32_fwdbwd"] = {"ms": round(ms, 4), "tflops": round(tf, 2),
+                                            "frac_mfma_f32": round(tf / MFMA_F32_PEAK_TFLOPS, 4)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -103,6 +167,7 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
     ap.add_argument("--precision", choices=["fp16", "fp32"], default="fp16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the S sweep / C2 / C4 extra configs")
     args = ap.parse_args()
 
     import torch
@@ -201,11 +266,19 @@ def main():
             "kernel_ms": {n: round(x, 4) for n, x in kms.items()}}
 
     cpu = None
+    extra = None
+    if rank == 0 and world == 1 and not args.no_extras:
+        extra = extras(fa2amd, torch, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(S, D)
         except Exception as e:  # the baseline is reported, never required
             log("cpu baseline failed:", e)
+        try:
+            if cpu is not None:
+                cpu["torch_sdpa_cpu"] = torch_sdpa_cpu(S, D, 16)
+        except Exception as e:
+            log("torch cpu baseline failed:", e)
 
     if rank == 0:
         line = {
@@ -227,6 +300,7 @@ def main():
             "hbm_gbps": round(hbm_bytes / elapsed / 1e9, 2),
             "roofline": roof,
             "cpu_baseline": cpu,
+            "extra_configs": extra,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -869,8 +869,10 @@ hipError_t dq_launch(const float* q, const float* k, const float* v, const float
 template <int D>
 hipError_t dq_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                        const float* delta, float* dq, int bh, int S, hipStream_t stream) {
-    const int nw = tune_knob("DQ_WAVES", 8);
-    if (nw == 8) return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, stream);
+    // 8 waves (2 per SIMD) for D <= 64; at D = 128 8 waves spill (~120 VGPRs), so 4
+    if constexpr (D <= 64) {
+        if (tune_knob("DQ_WAVES", 8) == 8) return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, stream);
+    }
     return dq_launch<D, 4>(q, k, v, dout, lse, delta, dq, bh, S, stream);
 }
 }  // namespace

@@ -224,20 +224,30 @@ __device__ __forceinline__ f32x16 splat16(float x) {
     return v;
 }
 
-// S^T of one 64-key tile (keys on registers, query on the lane), relative to m.
-template <int D, int ABL = 0>
-__device__ __forceinline__ void fwd_qk(f32x16 (&s)[2], const FwdState<D>& st, const _Float16* Ks,
+// S^T of one 64-key tile for the wave's MQ query groups (keys on registers, query
+// on the lane), relative to m.  Each K fragment read from LDS feeds MQ MFMAs.
+template <int D, int MQ, int ABL = 0>
+__device__ __forceinline__ void fwd_qk(f32x16 (&s)[MQ][2], const FwdState<D> (&st)[MQ], const _Float16* Ks,
                                        const FragOffsets<D>& fo) {
     if (ABL & 16) {
-        s[0] = st.nm + fo.rowop(Ks, 0, 0)[0];
-        s[1] = st.nm;
+#pragma unroll
+        for (int g = 0; g < MQ; ++g) {
+            s[g][0] = st[g].nm + fo.rowop(Ks, 0, 0)[0];
+            s[g][1] = st[g].nm;
+        }
         return;
     }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-        s[kb] = mfma(fo.rowop(Ks, kb * 32, 0), st.qf[0], st.nm);
+        const f16x8 a0 = fo.rowop(Ks, kb * 32, 0);
 #pragma unroll
-        for (int t = 1; t < D / 16; ++t) s[kb] = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], s[kb]);
+        for (int g = 0; g < MQ; ++g) s[g][kb] = mfma(a0, st[g].qf[0], st[g].nm);
+#pragma unroll
+        for (int t = 1; t < D / 16; ++t) {
+            const f16x8 a = fo.rowop(Ks, kb * 32, t);
+#pragma unroll
+            for (int g = 0; g < MQ; ++g) s[g][kb] = mfma(a, st[g].qf[t], s[g][kb]);
+        }
     }
 }
 
@@ -270,60 +280,69 @@ __device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[2], float sh, f16x8
         }
 }
 
-// Online softmax of one tile (sacc = s - m) and O^T += V^T P^T with the packed
-// scores as the B operand.  first: the wave's first tile (m := its row max).
-template <int D, bool MASK, int ABL = 0>
-__device__ __forceinline__ void fwd_softmax_pv(FwdState<D>& st, f32x16 (&sacc)[2], const _Float16* Vs,
+// Online softmax of one tile for the wave's MQ query groups (sacc = s - m) and
+// O^T += V^T P^T with the packed scores as the B operand (each V^T fragment feeds MQ
+// MFMAs).  first: the wave's first tile (m := its row max).  One slow-path decision
+// for all groups keeps the tile a single basic block on the common path.
+template <int D, int MQ, bool MASK, int ABL = 0>
+__device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&sacc)[MQ][2], const _Float16* Vs,
                                                const FragOffsets<D>& fo, int k0, int S, int h, bool first) {
     if (MASK) {  // ragged last tile only
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+        for (int g = 0; g < MQ; ++g)
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[kb][i] = -__builtin_inff();
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[g][kb][i] = -__builtin_inff();
     }
-    f16x8 pf[2][2];
-    float ls[4];
+    f16x8 pf[MQ][2][2];
+    float ls[MQ][4];
     bool slow = first;
     if (!first) {
-        fwd_exp<false, ABL>(sacc, 0.f, pf, ls);
-        const float ts = (ls[0] + ls[1]) + (ls[2] + ls[3]);
-        slow = !(ABL & 32) && __any(!(ts <= FA2_TILE_SUM_MAX));
+        bool bad = false;
+#pragma unroll
+        for (int g = 0; g < MQ; ++g) {
+            fwd_exp<false, ABL>(sacc[g], 0.f, pf[g], ls[g]);
+            const float ts = (ls[g][0] + ls[g][1]) + (ls[g][2] + ls[g][3]);
+            bad = bad || !(ts <= FA2_TILE_SUM_MAX);
+        }
+        slow = !(ABL & 32) && __any(bad);
     }
     if (slow) {
-        const float mx = xor32_max(tile_max(sacc));
-        const float d = first ? mx : fmaxf(mx, 0.f);
-        const float alpha = first ? 0.f : fast_exp2(-d);
-        st.m += d;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) st.l[c] *= alpha;
+        for (int g = 0; g < MQ; ++g) {
+            const float mx = xor32_max(tile_max(sacc[g]));
+            const float d = first ? mx : fmaxf(mx, 0.f);
+            const float alpha = first ? 0.f : fast_exp2(-d);
+            st[g].m += d;
 #pragma unroll
-        for (int b = 0; b < D / 32; ++b)
+            for (int c = 0; c < 4; ++c) st[g].l[c] *= alpha;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) st.oacc[b][i] *= alpha;
-        st.nm = splat16(-st.m);
-        fwd_exp<true, ABL>(sacc, d, pf, ls);
+            for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) st[g].oacc[b][i] *= alpha;
+            st[g].nm = splat16(-st[g].m);
+            fwd_exp<true, ABL>(sacc[g], d, pf[g], ls[g]);
+        }
     }
 #pragma unroll
-    for (int c = 0; c < 4; ++c) st.l[c] += ls[c];
+    for (int g = 0; g < MQ; ++g)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st[g].l[c] += ls[g][c];
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                if (ABL & 8) st.oacc[b][s + 2 * kb] += (float)pf[kb][s][b];
-                else st.oacc[b] = mfma(fo.trop(Vs, kb * 32 + 16 * s, b), pf[kb][s], st.oacc[b]);
+                const f16x8 v = fo.trop(Vs, kb * 32 + 16 * s, b);
+#pragma unroll
+                for (int g = 0; g < MQ; ++g) {
+                    if (ABL & 8) st[g].oacc[b][s + 2 * kb] += (float)pf[g][kb][s][b] + (float)v[0];
+                    else st[g].oacc[b] = mfma(v, pf[g][kb][s], st[g].oacc[b]);
+                }
             }
-}
-
-// One 64-key tile: QK^T, then softmax and PV.
-template <int D, bool MASK, int ABL = 0>
-__device__ __forceinline__ void fwd_tile(FwdState<D>& st, const _Float16* Ks, const _Float16* Vs,
-                                         const FragOffsets<D>& fo, int k0, int S, int h, bool first) {
-    f32x16 sacc[2];
-    fwd_qk<D, ABL>(sacc, st, Ks, fo);
-    fwd_softmax_pv<D, MASK, ABL>(st, sacc, Vs, fo, k0, S, h, first);
 }
 
 template <int D>
@@ -404,24 +423,28 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 #define FA2_STAMP_ARG
 #endif
 
-template <int D, int NW, int ABL = 0>
+// MQ 32-row query groups per wave (MQ = 2: two independent MFMA / softmax chains
+// per wave for the scheduler to interleave, each K / V^T fragment feeding two MFMAs).
+template <int D, int NW, int MQ, int ABL = 0>
 __global__ void __launch_bounds__(64 * NW)
 fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                    float* __restrict__ O, float* __restrict__ LSE, int S FA2_STAMP_ARG) {
     constexpr int KT = 64;  // keys per tile
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
+    constexpr int QW = 32 * MQ;  // query rows per wave
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];  // [buf][K | V]
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int nqb = (S + 32 * NW - 1) / (32 * NW);
+    const int nqb = (S + QW * NW - 1) / (QW * NW);
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = bid / nqb, qb = bid - bh * nqb;
     const long base = (long)bh * S * D;
-    const int q = qb * 32 * NW + wave * 32 + r;
+    const int q0 = qb * QW * NW + wave * QW + r;  // group g: query q0 + 32 g
 
-    FwdState<D> st;
-    fwd_init<D>(st, Q, base, q, S, h);
+    FwdState<D> st[MQ];
+#pragma unroll
+    for (int g = 0; g < MQ; ++g) fwd_init<D>(st[g], Q, base, q0 + 32 * g, S, h);
     FragOffsets<D> fo;
     fo.init(lane);
     TileStager<D, KT, NT> ks, vs;
@@ -448,15 +471,15 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                 vs.load((j + 1) * KT);
             }
             FA2_STAMP(0);
-            f32x16 sacc[2];
-            fwd_qk<D, ABL>(sacc, st, smem, fo);
+            f32x16 sacc[MQ][2];
+            fwd_qk<D, MQ, ABL>(sacc, st, smem, fo);
             if (more && FA2_FWD_LP) {
                 ks.load((j + 1) * KT);
                 vs.load((j + 1) * KT);
             }
             FA2_STAMP(1);
-            if (j == last_ragged) fwd_softmax_pv<D, true, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
-            else fwd_softmax_pv<D, false, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
+            if (j == last_ragged) fwd_softmax_pv<D, MQ, true, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
+            else fwd_softmax_pv<D, MQ, false, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
             FA2_STAMP(2);
             if (more) {
                 ks.store(smem + 2 * TILE, 1.f, tid);
@@ -473,16 +496,16 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                 vs.load((j + 2) * KT);
             }
             FA2_STAMP(0);
-            f32x16 sacc[2];
-            fwd_qk<D, ABL>(sacc, st, smem + 2 * TILE, fo);
+            f32x16 sacc[MQ][2];
+            fwd_qk<D, MQ, ABL>(sacc, st, smem + 2 * TILE, fo);
             if (more && FA2_FWD_LP) {
                 ks.load((j + 2) * KT);
                 vs.load((j + 2) * KT);
             }
             FA2_STAMP(1);
             if (j + 1 == last_ragged)
-                fwd_softmax_pv<D, true, ABL>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
-            else fwd_softmax_pv<D, false, ABL>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+                fwd_softmax_pv<D, MQ, true, ABL>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+            else fwd_softmax_pv<D, MQ, false, ABL>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
             FA2_STAMP(2);
             if (more) {
                 ks.store(smem, 1.f, tid);
@@ -497,7 +520,8 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     if (lane == 0)
         for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blockIdx.x * NW + wave) * FA2_NSTAMP + k] = stv[k];
 #endif
-    fwd_store<D>(st, O, LSE, base, (long)bh * S, q, S, h);
+#pragma unroll
+    for (int g = 0; g < MQ; ++g) fwd_store<D>(st[g], O, LSE, base, (long)bh * S, q0 + 32 * g, S, h);
 }
 
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
@@ -521,8 +545,8 @@ __device__ __forceinline__ void fwd_compat_body(const float* __restrict__ Q, con
     const int q = qb * 32 + r;
     _Float16* buf = lds + wave * KT * D;
 
-    FwdState<D> st;
-    fwd_init<D>(st, Q, base, q, S, h);
+    FwdState<D> st[1];
+    fwd_init<D>(st[0], Q, base, q, S, h);
     FragOffsets<D> fo;
     fo.init(lane);
     TileStager<D, KT, 64> ks, vs;
@@ -532,23 +556,23 @@ __device__ __forceinline__ void fwd_compat_body(const float* __restrict__ Q, con
     for (int j = wave; j < nt; j += 4) {
         ks.load(j * KT);
         ks.store(buf, 1.f, lane);
-        f32x16 sacc[2];
-        fwd_qk<D>(sacc, st, buf, fo);
+        f32x16 sacc[1][2];
+        fwd_qk<D, 1>(sacc, st, buf, fo);
         vs.load(j * KT);
         vs.store(buf, 1.f, lane);  // after this wave's K reads (in-order LDS within a wave)
-        if ((j + 1) * KT > S) fwd_softmax_pv<D, true>(st, sacc, buf, fo, j * KT, S, h, j == wave);
-        else fwd_softmax_pv<D, false>(st, sacc, buf, fo, j * KT, S, h, j == wave);
+        if ((j + 1) * KT > S) fwd_softmax_pv<D, 1, true>(st, sacc, buf, fo, j * KT, S, h, j == wave);
+        else fwd_softmax_pv<D, 1, false>(st, sacc, buf, fo, j * KT, S, h, j == wave);
     }
     // merge: O = sum_w 2^(m_w - M) O_w / sum_w 2^(m_w - M) l_w, M = max_w m_w
-    const float lw = xor32_sum((st.l[0] + st.l[1]) + (st.l[2] + st.l[3]));
+    const float lw = xor32_sum((st[0].l[0] + st[0].l[1]) + (st[0].l[2] + st[0].l[3]));
     __syncthreads();
     float* ow = reinterpret_cast<float*>(lds) + wave * 32 * D;  // [q][d] fp32 per wave
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) ow[r * D + 32 * b + (i & 3) + 8 * (i >> 2) + 4 * h] = st.oacc[b][i];
+        for (int i = 0; i < 16; ++i) ow[r * D + 32 * b + (i & 3) + 8 * (i >> 2) + 4 * h] = st[0].oacc[b][i];
     if (h == 0) {
-        mrg[0][wave][r] = wave < nt ? st.m : -__builtin_inff();
+        mrg[0][wave][r] = wave < nt ? st[0].m : -__builtin_inff();
         mrg[1][wave][r] = lw;
     }
     __syncthreads();
@@ -591,7 +615,7 @@ struct StampLog {
 static StampLog g_stamps;
 #endif
 
-template <int D, int NW, int ABL>
+template <int D, int NW, int MQ, int ABL>
 static void fwd_f16_go(const float* q, const float* k, const float* v, float* o, float* lse, long grid, int S,
                        hipStream_t stream) {
 #ifdef FA2_STAMPS
@@ -603,7 +627,7 @@ static void fwd_f16_go(const float* q, const float* k, const float* v, float* o,
         (void)hipMalloc(&buf, n * sizeof(unsigned long long));
         cap = n;
     }
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, MQ, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
                        v, o, lse, S, buf);
     std::vector<unsigned long long> h(n);
     (void)hipStreamSynchronize(stream);
@@ -611,28 +635,28 @@ static void fwd_f16_go(const float* q, const float* k, const float* v, float* o,
     for (long i = 0; i < n; ++i) g_stamps.sum[i % FA2_NSTAMP] += (double)h[i] / (grid * NW);
     ++g_stamps.launches;
 #else
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, MQ, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
                        v, o, lse, S);
 #endif
 }
 
-template <int D, int NW>
+template <int D, int NW, int MQ = 1>
 static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
                                  hipStream_t stream) {
-    const int nqb = (S + 32 * NW - 1) / (32 * NW);
+    const int nqb = (S + 32 * MQ * NW - 1) / (32 * MQ * NW);
     const long grid = (long)bh * nqb;
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
 #ifdef FA2_ABLATIONS
     switch (tune_knob("FWD_ABL", 0)) {
 #define FA2_FWD_ABL(X) \
-    case X: fwd_f16_go<D, NW, X>(q, k, v, o, lse, grid, S, stream); return hipGetLastError();
+    case X: fwd_f16_go<D, NW, MQ, X>(q, k, v, o, lse, grid, S, stream); return hipGetLastError();
         FA2_FWD_ABL(1) FA2_FWD_ABL(2) FA2_FWD_ABL(4) FA2_FWD_ABL(8) FA2_FWD_ABL(16) FA2_FWD_ABL(24) FA2_FWD_ABL(32)
         FA2_FWD_ABL(63) FA2_FWD_ABL(64)
 #undef FA2_FWD_ABL
         default: break;
     }
 #endif
-    fwd_f16_go<D, NW, 0>(q, k, v, o, lse, grid, S, stream);
+    fwd_f16_go<D, NW, MQ, 0>(q, k, v, o, lse, grid, S, stream);
     return hipGetLastError();
 }
 
@@ -641,6 +665,8 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
                                    hipStream_t stream) {
     // 8 waves (2 per SIMD) where the registers allow it; D = 128 runs 4 waves of
     // ~400 VGPRs (8 would spill and exceed the LDS budget with the Q stages)
+    // (MQ = 2, two 32-row query groups per wave at 4 waves / 1 per SIMD, measured
+    // 30 % slower than 8 waves x 1 group at D = 32 and 64 -- r01)
     if constexpr (D <= 64) {
         if (tune_knob("FWD_WAVES", 8) == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
     }
