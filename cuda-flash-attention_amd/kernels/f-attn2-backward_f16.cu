@@ -174,6 +174,46 @@ struct TileStager {
     }
 };
 
+// Row-coalesced prologue / epilogue (FA2_BWD_COAL).  A workgroup's stationary
+// operand block (K and V for dK/dV, Q and dO for dQ) is one contiguous HBM range:
+// it is loaded whole rows at a time into the (still idle) LDS tile buffers as scaled
+// fp16 and read back as B fragments, instead of every lane fetching 16-B pieces of
+// its own row (32 rows per instruction).  Results leave through a wave-private LDS
+// stage as whole 128-B row segments.
+#ifndef FA2_BWD_COAL
+#define FA2_BWD_COAL 1
+#endif
+
+template <int D, int ROWS, int NT>
+__device__ __forceinline__ void stage_block(_Float16* lds, const float* head_base, int S, int row0, float scale,
+                                            int tid) {
+    TileStager<D, ROWS, NT> st;
+    st.init(head_base, S, tid);
+    st.load(row0);
+    st.store(lds, scale, tid);
+}
+
+// a wave's 32 x D accumulator block (row d = 32b + (i&3) + 8(i>>2) + 4h of the
+// transposed result, column = lane & 31 = output row) -> rows [0, rows_valid) of dst
+template <int D>
+__device__ __forceinline__ void store_block_rows(float (*os)[36], const f32x16 (&acc)[D / 32], float scale,
+                                                 float* __restrict__ dst, int rows_valid, int lane) {
+    const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) os[r][(i & 3) + 8 * (i >> 2) + 4 * h] = acc[b][i] * scale;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const int row = 8 * s4 + (lane >> 3), c4 = (lane & 7) * 4;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(&os[row][c4]);
+            if (row < rows_valid) *reinterpret_cast<f32x4*>(dst + (long)row * D + 32 * b + c4) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // dK, dV:  grid BH * ceil(S / (32*NW)), block 64*NW
 // ---------------------------------------------------------------------------
@@ -303,6 +343,9 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     // [buf][Q | dO] fp16 tiles, then [buf][-lse2 | -delta] fp32 rows
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
     __shared__ __attribute__((aligned(16))) float rows[2][2][QT];
+#if FA2_BWD_COAL
+    __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];  // per-wave result stage
+#endif
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int nkb = (S + KPW * NW - 1) / (KPW * NW);
@@ -314,14 +357,37 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
 
     DkdvState<D, KB> st;
+    FragOffsets<D> fo;
+    fo.init(lane);
+    (void)r;
+#if FA2_BWD_COAL
+    static_assert(KPW * NW <= 4 * QT, "K / V block fits the Q/dO buffers");
+    const int kblock0 = kblk * KPW * NW;
+    stage_block<D, KPW * NW, NT>(smem, K + base, S, kblock0, kscale, tid);
+    __syncthreads();
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) st.kf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
+    __syncthreads();
+    stage_block<D, KPW * NW, NT>(smem, V + base, S, kblock0, 1.f, tid);
+    __syncthreads();
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) st.vf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
+    __syncthreads();
+#endif
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
+#if !FA2_BWD_COAL
         const int key = key0 + kb * 32 + r;
 #pragma unroll
         for (int t = 0; t < D / 16; ++t) {
             st.kf[kb][t] = load_frag(K + base + (long)key * D + 16 * t + 8 * h, key < S, kscale);
             st.vf[kb][t] = load_frag(V + base + (long)key * D + 16 * t + 8 * h, key < S, 1.f);
         }
+#endif
 #pragma unroll
         for (int b = 0; b < D / 32; ++b)
 #pragma unroll
@@ -331,8 +397,6 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
             }
     }
 
-    FragOffsets<D> fo;
-    fo.init(lane);
     TileStager<D, QT, NT> qs, dos;
     qs.init(Q + base, S, tid);
     dos.init(dO + base, S, tid);
@@ -430,6 +494,14 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
 #endif
 
     const float dscale = 1.f / __builtin_sqrtf((float)D);
+#if FA2_BWD_COAL
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+        const int k0r = key0 + kb * 32;
+        store_block_rows<D>(ostage[wave], st.dka[kb], dscale, dK + base + (long)k0r * D, S - k0r, lane);
+        store_block_rows<D>(ostage[wave], st.dva[kb], 1.f, dV + base + (long)k0r * D, S - k0r, lane);
+    }
+#else
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
         const int key = key0 + kb * 32 + r;
@@ -449,6 +521,7 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
                 }
         }
     }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -502,6 +575,9 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
+#if FA2_BWD_COAL
+    __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];  // per-wave dQ stage
+#endif
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int nqb = (S + 32 * NW - 1) / (32 * NW);
@@ -513,11 +589,27 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     const float qscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
 
     DqState<D> st;
+    FragOffsets<D> fo;
+    fo.init(lane);
+#if FA2_BWD_COAL
+    static_assert(32 * NW <= 4 * KT, "Q / dO block fits the K/V buffers");
+    stage_block<D, 32 * NW, NT>(smem, Q + base, S, qb * 32 * NW, qscale, tid);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) st.qf[t] = fo.rowop(smem, wave * 32, t);
+    __syncthreads();
+    stage_block<D, 32 * NW, NT>(smem, dO + base, S, qb * 32 * NW, 1.f, tid);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) st.df[t] = fo.rowop(smem, wave * 32, t);
+    __syncthreads();
+#else
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
         st.qf[t] = load_frag(Q + base + (long)q * D + 16 * t + 8 * h, qvalid, qscale);
         st.df[t] = load_frag(dO + base + (long)q * D + 16 * t + 8 * h, qvalid, 1.f);
     }
+#endif
     {
         const float nl = qvalid ? -LSE[(long)bh * S + q] * FA2B_LOG2E : -__builtin_inff();
         const float nd = qvalid ? -Delta[(long)bh * S + q] : 0.f;
@@ -532,8 +624,6 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 #pragma unroll
         for (int i = 0; i < 16; ++i) st.dqa[b][i] = 0.f;
 
-    FragOffsets<D> fo;
-    fo.init(lane);
     TileStager<D, KT, NT> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
@@ -585,6 +675,13 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
         }
     }
 
+#if FA2_BWD_COAL
+    {
+        const int q0w = qb * 32 * NW + wave * 32;
+        store_block_rows<D>(ostage[wave], st.dqa, 1.f / __builtin_sqrtf((float)D), dQ + base + (long)q0w * D, S - q0w,
+                            lane);
+    }
+#else
     if (qvalid) {
         const float dscale = 1.f / __builtin_sqrtf((float)D);
         float* row = dQ + base + (long)q * D;
@@ -597,6 +694,7 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
                 *reinterpret_cast<f32x4*>(row + 32 * b + 8 * g + 4 * h) = a;
             }
     }
+#endif
 }
 
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
@@ -850,7 +948,6 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
 #endif
     if constexpr (D <= 64) {
         if (kbk == 2) {
-            if (D == 32 && nw == 8) return dkdv_launch<D, 8, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
             return dkdv_launch<D, 4, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
         }
         if (nw == 8) return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);

@@ -402,6 +402,10 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 #ifndef FA2_FWD_LP
 #define FA2_FWD_LP 1
 #endif
+// FA2_FWD_COAL: Q loaded and O stored as whole rows through LDS (prologue/epilogue)
+#ifndef FA2_FWD_COAL
+#define FA2_FWD_COAL 1
+#endif
 
 // FA2_STAMPS (diagnostic builds only): s_memtime at the loop's segment boundaries,
 // per-wave sums written to `stamps` (read the shares, never the build's run time:
@@ -434,6 +438,9 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     constexpr int TILE = KT * D;
     constexpr int QW = 32 * MQ;  // query rows per wave
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];  // [buf][K | V]
+#if FA2_FWD_COAL
+    __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];  // per-wave O block stage
+#endif
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int nqb = (S + QW * NW - 1) / (QW * NW);
@@ -443,10 +450,31 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     const int q0 = qb * QW * NW + wave * QW + r;  // group g: query q0 + 32 g
 
     FwdState<D> st[MQ];
-#pragma unroll
-    for (int g = 0; g < MQ; ++g) fwd_init<D>(st[g], Q, base, q0 + 32 * g, S, h);
     FragOffsets<D> fo;
     fo.init(lane);
+#if FA2_FWD_COAL
+    // Q block (32*MQ*NW rows, one contiguous HBM range) loaded row-coalesced, converted
+    // and scaled into the (still idle) K/V LDS buffers, then read back as this wave's
+    // B fragments: 1 KB per load instruction instead of 32 rows x 32 B per-lane pieces.
+    static_assert(32 * MQ * NW <= 4 * KT, "Q block fits the K/V buffers");
+    {
+        TileStager<D, 32 * MQ * NW, NT> qst;
+        qst.init(Q + base, S, tid);
+        qst.load(qb * QW * NW);
+        qst.store(smem, FA2_LOG2E / __builtin_sqrtf((float)D), tid);
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < MQ; ++g) {
+            fwd_init<D>(st[g], nullptr, 0, S, S, h);  // state only (q >= S: no Q read)
+#pragma unroll
+            for (int t = 0; t < D / 16; ++t) st[g].qf[t] = fo.rowop(smem, wave * QW + 32 * g, t);
+        }
+        __syncthreads();
+    }
+#else
+#pragma unroll
+    for (int g = 0; g < MQ; ++g) fwd_init<D>(st[g], Q, base, q0 + 32 * g, S, h);
+#endif
     TileStager<D, KT, NT> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
@@ -520,8 +548,34 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     if (lane == 0)
         for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blockIdx.x * NW + wave) * FA2_NSTAMP + k] = stv[k];
 #endif
+#if FA2_FWD_COAL
+    // O through a wave-private LDS stage, one 32x32 block at a time, stored as whole
+    // 128-B row segments (8 rows per instruction) instead of 16-B pieces of 32 rows
+#pragma unroll
+    for (int g = 0; g < MQ; ++g) {
+        const float lt = xor32_sum((st[g].l[0] + st[g].l[1]) + (st[g].l[2] + st[g].l[3]));
+        const float inv = 1.f / lt;
+        const int qrow0 = qb * QW * NW + wave * QW + 32 * g;  // first row of this group
+        float(*os)[36] = ostage[wave];
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) os[r][(i & 3) + 8 * (i >> 2) + 4 * h] = st[g].oacc[b][i] * inv;
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int row = 8 * s4 + (lane >> 3), c4 = (lane & 7) * 4;
+                const f32x4 v = *reinterpret_cast<const f32x4*>(&os[row][c4]);
+                if (qrow0 + row < S) *reinterpret_cast<f32x4*>(O + base + (long)(qrow0 + row) * D + 32 * b + c4) = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (h == 0 && q0 + 32 * g < S) LSE[(long)bh * S + q0 + 32 * g] = st[g].m * FA2_LN2 + __logf(lt);
+    }
+#else
 #pragma unroll
     for (int g = 0; g < MQ; ++g) fwd_store<D>(st[g], O, LSE, base, (long)bh * S, q0 + 32 * g, S, h);
+#endif
 }
 
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
