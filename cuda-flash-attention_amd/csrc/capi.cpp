@@ -136,6 +136,15 @@ int fa2_backward_dq(const float* q, const float* k, const float* v, const float*
         "fa2_backward_dq launch");
 }
 
+int fa2_backward_dq_delta(const float* q, const float* k, const float* v, const float* o, const float* dout,
+                          const float* lse, float* delta, float* dq, int B, int H, int S, int D, void* stream) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_ptrs({q, k, v, o, dout, lse, delta, dq}))) return rc;
+    return hip_status(fa2::launch_bwd_dq_delta_f16(D, q, k, v, o, dout, lse, delta, dq, B * H, S,
+                                                   static_cast<hipStream_t>(stream)),
+                      "fa2_backward_dq_delta launch");
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

@@ -28,7 +28,7 @@ SUPPORTED_HEAD_DIMS = (32, 64, 128)
 
 # exported symbols of include/fa2_amd.h (checked by tests/test_capi_symbols.py)
 C_SYMBOLS = (
-    "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv", "fa2_backward_dq",
+    "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv", "fa2_backward_dq", "fa2_backward_dq_delta",
     "fa2_forward_host", "fa2_backward_host", "fa2_shard_range", "fa2_last_error",
     "fa2_version", "fa2_device_count",
 )
@@ -82,6 +82,7 @@ def _load(path):
         "fa2_backward": [P] * 10 + [I] * 5 + [V],
         "fa2_backward_dkdv": [P] * 8 + [I] * 4 + [V],
         "fa2_backward_dq": [P] * 7 + [I] * 4 + [V],
+        "fa2_backward_dq_delta": [P] * 8 + [I] * 4 + [V],
         "fa2_forward_host": [P] * 5 + [I] * 6 + [FP],
         "fa2_backward_host": [P] * 9 + [I] * 6 + [FP],
         "fa2_shard_range": [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)],
@@ -197,6 +198,14 @@ def backward_dq(q, k, v, dout, lse, delta_buf, dq, stream=None):
     ptrs = [_dev(t, n) for t, n in zip((q, k, v, dout, lse, delta_buf, dq),
                                        ("q", "k", "v", "dout", "lse", "delta", "dq"))]
     _check(lib().fa2_backward_dq(*ptrs, B, H, S, D, _stream(stream, q.device)))
+
+
+def backward_dq_delta(q, k, v, o, dout, lse, delta_buf, dq, stream=None):
+    """dQ with Δ = rowsum(dO * O) computed in the same kernel and written to delta_buf."""
+    B, H, S, D = _shape(q)
+    ptrs = [_dev(t, n) for t, n in zip((q, k, v, o, dout, lse, delta_buf, dq),
+                                       ("q", "k", "v", "o", "dout", "lse", "delta", "dq"))]
+    _check(lib().fa2_backward_dq_delta(*ptrs, B, H, S, D, _stream(stream, q.device)))
 
 
 # ---------------------------------------------------------------------------

@@ -193,6 +193,36 @@ __device__ __forceinline__ void stage_block(_Float16* lds, const float* head_bas
     st.store(lds, scale, tid);
 }
 
+// dO block -> fp16 LDS (as stage_block) and, fused, Δ = rowsum(dO ∘ O) of the
+// block's rows from the same row-coalesced registers: the CPR threads that hold one
+// row's chunks are consecutive lanes, reduced with xor shuffles.  Δ goes to
+// `delta_lds` (this workgroup's rows) and to HBM for the dK/dV kernel.
+template <int D, int ROWS, int NT>
+__device__ __forceinline__ void stage_block_delta(_Float16* lds, const float* dO_head, const float* O_head, int S,
+                                                  int row0, float* delta_lds, float* __restrict__ delta_out,
+                                                  int tid) {
+    using TS = TileStager<D, ROWS, NT>;
+    TS a, o;
+    a.init(dO_head, S, tid);
+    o.init(O_head, S, tid);
+    a.load(row0);
+    o.load(row0);
+    a.store(lds, 1.f, tid);
+#pragma unroll
+    for (int c = 0; c < TS::CPT; ++c) {
+        const int x = tid + c * NT;
+        const f32x4 p0 = a.r[c][0] * o.r[c][0], p1 = a.r[c][1] * o.r[c][1];
+        float d = ((p0[0] + p0[1]) + (p0[2] + p0[3])) + ((p1[0] + p1[1]) + (p1[2] + p1[3]));
+#pragma unroll
+        for (int off = TS::CPR / 2; off > 0; off >>= 1) d += __shfl_xor(d, off);
+        const int row = x / TS::CPR;
+        if ((TS::EXACT || x < TS::CHUNKS) && x % TS::CPR == 0) {
+            delta_lds[row] = d;
+            if (row0 + row < S) delta_out[row0 + row] = d;
+        }
+    }
+}
+
 // a wave's 32 x D accumulator block (row d = 32b + (i&3) + 8(i>>2) + 4h of the
 // transposed result, column = lane & 31 = output row) -> rows [0, rows_valid) of dst
 template <int D>
@@ -566,11 +596,13 @@ __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, cons
             for (int s = 0; s < 2; ++s) st.dqa[b] = mfma(fo.trop(Ks, kb * 32 + 16 * s, b), dsf[kb][s], st.dqa[b]);
 }
 
-template <int D, int NW>
+// DELTA: Δ is computed here (from O, fused into the dO prologue) and written to
+// `Delta` for the dK/dV kernel, which then runs after this one.
+template <int D, int NW, bool DELTA = false>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                      const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-                      float* __restrict__ dQ, int S) {
+                      const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
+                      float* __restrict__ dQ, int S, const float* __restrict__ O) {
     constexpr int KT = 64;
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
@@ -598,7 +630,11 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) st.qf[t] = fo.rowop(smem, wave * 32, t);
     __syncthreads();
-    stage_block<D, 32 * NW, NT>(smem, dO + base, S, qb * 32 * NW, 1.f, tid);
+    __shared__ float delta_blk[DELTA ? 32 * NW : 1];
+    if (DELTA)
+        stage_block_delta<D, 32 * NW, NT>(smem, dO + base, O + base, S, qb * 32 * NW, delta_blk,
+                                          Delta + (long)bh * S, tid);
+    else stage_block<D, 32 * NW, NT>(smem, dO + base, S, qb * 32 * NW, 1.f, tid);
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) st.df[t] = fo.rowop(smem, wave * 32, t);
@@ -612,7 +648,11 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 #endif
     {
         const float nl = qvalid ? -LSE[(long)bh * S + q] * FA2B_LOG2E : -__builtin_inff();
+#if FA2_BWD_COAL
+        const float nd = !qvalid ? 0.f : DELTA ? -delta_blk[wave * 32 + r] : -Delta[(long)bh * S + q];
+#else
         const float nd = qvalid ? -Delta[(long)bh * S + q] : 0.f;
+#endif
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             st.nlse2[i] = nl;
@@ -956,21 +996,27 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
 }
 template <int D, int NW>
 hipError_t dq_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
-                     const float* delta, float* dq, int bh, int S, hipStream_t stream) {
+                     float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
     const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q,
-                       k, v, dout, lse, delta, dq, S);
+#if FA2_BWD_COAL
+    if (o)
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true>), dim3((unsigned)grid), dim3(64 * NW), 0,
+                           stream, q, k, v, dout, lse, delta, dq, S, o);
+    else
+#endif
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false>), dim3((unsigned)grid), dim3(64 * NW), 0,
+                           stream, q, k, v, dout, lse, delta, dq, S, o);
     return hipGetLastError();
 }
 template <int D>
 hipError_t dq_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
-                       const float* delta, float* dq, int bh, int S, hipStream_t stream) {
+                       float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
     // 8 waves (2 per SIMD) for D <= 64; at D = 128 8 waves spill (~120 VGPRs), so 4
     if constexpr (D <= 64) {
-        if (tune_knob("DQ_WAVES", 8) == 8) return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, stream);
+        if (tune_knob("DQ_WAVES", 8) == 8) return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
     }
-    return dq_launch<D, 4>(q, k, v, dout, lse, delta, dq, bh, S, stream);
+    return dq_launch<D, 4>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
 }
 }  // namespace
 
@@ -989,22 +1035,34 @@ hipError_t launch_bwd_dkdv_f16(int D, const float* q, const float* k, const floa
 hipError_t launch_bwd_dq_f16(int D, const float* q, const float* k, const float* v, const float* dout,
                              const float* lse, const float* delta, float* dq, int bh, int S, hipStream_t stream) {
     if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
+    float* dl = const_cast<float*>(delta);  // read only when o == nullptr
     switch (D) {
-        case 32: return dq_dispatch<32>(q, k, v, dout, lse, delta, dq, bh, S, stream);
-        case 64: return dq_dispatch<64>(q, k, v, dout, lse, delta, dq, bh, S, stream);
-        case 128: return dq_dispatch<128>(q, k, v, dout, lse, delta, dq, bh, S, stream);
+        case 32: return dq_dispatch<32>(q, k, v, dout, lse, dl, dq, bh, S, nullptr, stream);
+        case 64: return dq_dispatch<64>(q, k, v, dout, lse, dl, dq, bh, S, nullptr, stream);
+        case 128: return dq_dispatch<128>(q, k, v, dout, lse, dl, dq, bh, S, nullptr, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
+hipError_t launch_bwd_dq_delta_f16(int D, const float* q, const float* k, const float* v, const float* o,
+                                   const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
+                                   hipStream_t stream) {
+    if (bh <= 0 || S <= 0 || !o) return hipErrorInvalidValue;
+    switch (D) {
+        case 32: return dq_dispatch<32>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        case 64: return dq_dispatch<64>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        case 128: return dq_dispatch<128>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// Δ fused into the dQ kernel's prologue (which stages dO anyway); dK/dV reads it.
 hipError_t launch_backward_f16(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream) {
-    hipError_t e = launch_delta(D, dout, o, delta, bh, S, stream);
+    hipError_t e = launch_bwd_dq_delta_f16(D, q, k, v, o, dout, lse, delta, dq, bh, S, stream);
     if (e != hipSuccess) return e;
-    e = launch_bwd_dkdv_f16(D, q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-    if (e != hipSuccess) return e;
-    return launch_bwd_dq_f16(D, q, k, v, dout, lse, delta, dq, bh, S, stream);
+    return launch_bwd_dkdv_f16(D, q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
 
 }  // namespace fa2

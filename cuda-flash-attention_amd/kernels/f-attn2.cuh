@@ -77,6 +77,11 @@ hipError_t launch_bwd_dkdv_f16(int D, const float* q, const float* k, const floa
                                hipStream_t stream);
 hipError_t launch_bwd_dq_f16(int D, const float* q, const float* k, const float* v, const float* dout,
                              const float* lse, const float* delta, float* dq, int bh, int S, hipStream_t stream);
+// dQ with Δ = rowsum(dO * O) computed in its prologue and written to `delta` (the
+// dK/dV kernel, launched after it, reads that); replaces launch_delta + dQ
+hipError_t launch_bwd_dq_delta_f16(int D, const float* q, const float* k, const float* v, const float* o,
+                                   const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
+                                   hipStream_t stream);
 
 inline bool supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 

@@ -66,6 +66,12 @@ int fa2_backward_dkdv(const float* q, const float* k, const float* v, const floa
                       void* stream);
 int fa2_backward_dq(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                     const float* delta, float* dq, int batch, int heads, int seq, int head_dim, void* stream);
+/* dQ with Δ computed in the same kernel (from O and dO) and written to `delta`
+ * (B*H*S floats); fa2_backward_dkdv launched after it reads that Δ.  This pair is
+ * what fa2_backward runs for FA2_FP16 (fp16 tiles only). */
+int fa2_backward_dq_delta(const float* q, const float* k, const float* v, const float* o, const float* dout,
+                          const float* lse, float* delta, float* dq, int batch, int heads, int seq, int head_dim,
+                          void* stream);
 
 /* ---------------------------------------------------------------------------
  * Host-pointer API: the reference host functions' semantics

@@ -49,6 +49,10 @@ def test_invalid_arguments_rejected_without_device():
     # null pointer
     rc = L.fa2_backward(one, one, one, one, one, one, one, one, null, one, 1, 1, 8, 64, fa2amd.FA2_FP32, null)
     assert rc == -1 and b"null" in L.fa2_last_error()
+    rc = L.fa2_backward_dq_delta(one, one, one, null, one, one, one, one, 1, 1, 8, 64, null)
+    assert rc == -1 and b"null" in L.fa2_last_error()
+    rc = L.fa2_backward_dq_delta(one, one, one, one, one, one, one, one, 1, 1, 8, 96, null)
+    assert rc == -1 and b"head_dim" in L.fa2_last_error()
     # non-positive sizes
     assert L.fa2_delta(one, one, one, 0, 1, 8, 64, null) == -1
 

@@ -35,7 +35,8 @@ def main():
     o, lse = fa2amd.forward(q, k, v, "fp16")
     dl = fa2amd.delta(do, o)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
-    flops = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "delta": 0.0, "bwd": 10.0, "step": 14.0}
+    flops = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "dqd": 2.0, "delta": 0.0, "bwd": 10.0, "step": 14.0,
+             "step3": 14.0}
     calls = {
         "fwd": lambda: fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
         "dkdv": lambda: fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv),
@@ -43,9 +44,14 @@ def main():
         "delta": lambda: fa2amd.delta(do, o, out=dl),
         "bwd": lambda: fa2amd.backward(q, k, v, o, do, lse, "fp16", dq=dq, dk=dk, dv=dv, delta_buf=dl),
         # one bench.py step: fwd, delta, dK/dV, dQ in stream order
-        "step": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse), fa2amd.delta(do, o, out=dl),
-                         fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv),
-                         fa2amd.backward_dq(q, k, v, do, lse, dl, dq)),
+        "step": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
+                         fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
+                         fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv)),
+        "dqd": lambda: fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
+        # the pre-fusion order: separate delta kernel, dK/dV, dQ
+        "step3": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse), fa2amd.delta(do, o, out=dl),
+                          fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv),
+                          fa2amd.backward_dq(q, k, v, do, lse, dl, dq)),
     }
     kernels = args.kernel or ["fwd", "dkdv", "dq"]
     variants = args.variant or [""]
