@@ -146,6 +146,7 @@ struct TileStager {
     f32x4 r[CPT][2];
     int voff[CPT], loff[CPT];
     __amdgpu_buffer_rsrc_t rs;
+    bool on = true;  // wave-uniform: this wave takes part in the staging
 
     __device__ __forceinline__ void init(const float* head_base, int S, int tid) {
         rs = head_rsrc(head_base, S, D);
@@ -159,6 +160,7 @@ struct TileStager {
     }
     // rows [row0, row0 + ROWS); rows >= S read as zeros
     __device__ __forceinline__ void load(int row0) {
+        if (!on) return;
         const int soff = row0 * D * 4;
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
@@ -167,6 +169,7 @@ struct TileStager {
         }
     }
     __device__ __forceinline__ void store(_Float16* tile, float scale, int tid) const {
+        if (!on) return;
 #pragma unroll
         for (int c = 0; c < CPT; ++c)
             if (EXACT || tid + c * NT < CHUNKS)
@@ -335,6 +338,12 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
 #ifndef FA2_DKDV_LP
 #define FA2_DKDV_LP 1
 #endif
+#ifndef FA2_DKDV_SW
+#define FA2_DKDV_SW 4
+#endif
+#ifndef FA2_DQ_SW
+#define FA2_DQ_SW 0
+#endif
 #ifndef FA2_DQ_LP
 #define FA2_DQ_LP 1
 #endif
@@ -427,7 +436,14 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
             }
     }
 
-    TileStager<D, QT, NT> qs, dos;
+    // Staging of the next Q/dO step is done by the first FA2_DKDV_SW waves only (all
+    // NW when 0): stamps showed waves NW/2..NW-1 (which lose VALU arbitration to their
+    // SIMD partners) ~15 % slower per step and the first half idling at the barrier,
+    // so the staging work goes to the first half.
+    constexpr int SW = (FA2_DKDV_SW > 0 && FA2_DKDV_SW < NW) ? FA2_DKDV_SW : NW;
+    constexpr int NS = 64 * SW;
+    const bool stg = __builtin_amdgcn_readfirstlane(wave) < SW;
+    TileStager<D, QT, NS> qs, dos;
     qs.init(Q + base, S, tid);
     dos.init(dO + base, S, tid);
     // Row constants of the staged step: wave 0 carries LSE, wave 1 carries Delta
@@ -456,26 +472,33 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     // 0 = all at the step start, 1 = all between the two query blocks, 2 = Q at the
     // start and dO + row constants between the blocks
     auto load_a = [&](int it) {
-        if (FA2_DKDV_LP == 0 || FA2_DKDV_LP == 2) qs.load(it * QT);
+        if ((FA2_DKDV_LP == 0 || FA2_DKDV_LP == 2) && stg) qs.load(it * QT);
         if (FA2_DKDV_LP == 0) {
-            dos.load(it * QT);
+            if (stg) dos.load(it * QT);
             load_rows(it * QT);
         }
     };
     auto load_b = [&](int it) {
-        if (FA2_DKDV_LP == 1) qs.load(it * QT);
+        if (FA2_DKDV_LP == 1 && stg) qs.load(it * QT);
         if (FA2_DKDV_LP != 0) {
-            dos.load(it * QT);
+            if (stg) dos.load(it * QT);
             load_rows(it * QT);
         }
     };
+    auto store_step = [&](_Float16* qdst, _Float16* ddst, int rbuf) {
+        if (stg) {
+            qs.store(qdst, 1.f, tid);
+            dos.store(ddst, 1.f, tid);
+        }
+        store_rows(rbuf);
+    };
     const int nsteps = (S + QT - 1) / QT;
-    qs.load(0);
-    dos.load(0);
+    if (stg) {
+        qs.load(0);
+        dos.load(0);
+    }
     load_rows(0);
-    qs.store(smem, 1.f, tid);
-    dos.store(smem + TILE, 1.f, tid);
-    store_rows(0);
+    store_step(smem, smem + TILE, 0);
     __syncthreads();
 
 #ifdef FA2_STAMPS
@@ -491,11 +514,7 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
                 if (more) load_b(it + 1);
             });
             FA2_STAMP(1);
-            if (more) {
-                qs.store(smem + 2 * TILE, 1.f, tid);
-                dos.store(smem + 3 * TILE, 1.f, tid);
-                store_rows(1);
-            }
+            if (more) store_step(smem + 2 * TILE, smem + 3 * TILE, 1);
             FA2_STAMP(2);
             if (!(ABL & 4)) __syncthreads();
             FA2_STAMP(3);
@@ -508,11 +527,7 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
                 if (more) load_b(it + 2);
             });
             FA2_STAMP(1);
-            if (more) {
-                qs.store(smem, 1.f, tid);
-                dos.store(smem + TILE, 1.f, tid);
-                store_rows(0);
-            }
+            if (more) store_step(smem, smem + TILE, 0);
             FA2_STAMP(2);
             if (!(ABL & 4)) __syncthreads();
             FA2_STAMP(3);
@@ -664,9 +679,12 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 #pragma unroll
         for (int i = 0; i < 16; ++i) st.dqa[b][i] = 0.f;
 
-    TileStager<D, KT, NT> ks, vs;
+    // K/V staging by the first FA2_DQ_SW waves (all when 0), as in the dK/dV kernel
+    constexpr int SW = (FA2_DQ_SW > 0 && FA2_DQ_SW < NW) ? FA2_DQ_SW : NW;
+    TileStager<D, KT, 64 * SW> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
+    ks.on = vs.on = __builtin_amdgcn_readfirstlane(wave) < SW;
     const int ntiles = (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     ks.load(0);

@@ -153,6 +153,7 @@ struct TileStager {
     f32x4 r[CPT][2];
     int voff[CPT], loff[CPT];
     __amdgpu_buffer_rsrc_t rs;
+    bool on = true;  // wave-uniform: this wave takes part in the staging
 
     __device__ __forceinline__ void set_head(const float* head_base, int S) { rs = head_rsrc(head_base, S, D); }
     __device__ __forceinline__ void init(const float* head_base, int S, int tid) {
@@ -167,6 +168,7 @@ struct TileStager {
     }
     // rows [row0, row0 + ROWS); rows >= S read as zeros
     __device__ __forceinline__ void load(int row0) {
+        if (!on) return;
         const int soff = row0 * D * 4;
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
@@ -175,6 +177,7 @@ struct TileStager {
         }
     }
     __device__ __forceinline__ void store(_Float16* tile, float scale, int tid) const {
+        if (!on) return;
 #pragma unroll
         for (int c = 0; c < CPT; ++c)
             if (EXACT || tid + c * NT < CHUNKS)
@@ -402,6 +405,9 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 #ifndef FA2_FWD_LP
 #define FA2_FWD_LP 1
 #endif
+#ifndef FA2_FWD_SW
+#define FA2_FWD_SW 0
+#endif
 // FA2_FWD_COAL: Q loaded and O stored as whole rows through LDS (prologue/epilogue)
 #ifndef FA2_FWD_COAL
 #define FA2_FWD_COAL 1
@@ -475,9 +481,13 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
 #pragma unroll
     for (int g = 0; g < MQ; ++g) fwd_init<D>(st[g], Q, base, q0 + 32 * g, S, h);
 #endif
-    TileStager<D, KT, NT> ks, vs;
+    // K/V staging by the first FA2_FWD_SW waves (all when 0): the second half loses
+    // VALU arbitration to its SIMD partners, so the first half takes the staging
+    constexpr int SW = (FA2_FWD_SW > 0 && FA2_FWD_SW < NW) ? FA2_FWD_SW : NW;
+    TileStager<D, KT, 64 * SW> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
+    ks.on = vs.on = __builtin_amdgcn_readfirstlane(wave) < SW;
     const int ntiles = (ABL & 64) ? 1 : (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     ks.load(0);
