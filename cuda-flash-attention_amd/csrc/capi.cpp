@@ -63,6 +63,22 @@ int tune_knob(const char* name, int dflt) {
     const char* v = getenv(key.c_str());
     return v ? atoi(v) : dflt;
 }
+
+int auto_waves(long blocks32, int maxnw, int minnw) {
+    static int ncu_cache[64] = {};
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        if (!ncu_cache[dev]) {
+            int n = 0;
+            if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+                ncu_cache[dev] = n;
+        }
+        if (ncu_cache[dev]) ncu = ncu_cache[dev];
+    }
+    for (int nw = maxnw; nw > minnw; nw /= 2)
+        if ((blocks32 + nw - 1) / nw >= ncu) return nw;
+    return minnw;
+}
 }  // namespace fa2
 
 extern "C" {

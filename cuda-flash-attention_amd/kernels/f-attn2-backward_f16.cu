@@ -990,7 +990,9 @@ hipError_t dkdv_launch(const float* q, const float* k, const float* v, const flo
 template <int D>
 hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                          const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-    const int nw = tune_knob("DKDV_WAVES", D <= 64 ? 8 : 4);
+    // FA2_TUNE_DKDV_WAVES = 0 (default): auto_waves over the grid of 32-key wave units
+    int nw = tune_knob("DKDV_WAVES", 0);
+    if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), D <= 64 ? 8 : 4);
     const int kbk = tune_knob("DKDV_KB", 1);
 #ifdef FA2_ABLATIONS
     if constexpr (D == 64) {
@@ -1010,6 +1012,7 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
         }
         if (nw == 8) return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     }
+    if (nw == 2) return dkdv_launch<D, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
 template <int D, int NW>
@@ -1031,8 +1034,12 @@ template <int D>
 hipError_t dq_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                        float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
     // 8 waves (2 per SIMD) for D <= 64; at D = 128 8 waves spill (~120 VGPRs), so 4
+    // FA2_TUNE_DQ_WAVES = 0 (default): auto_waves over the grid of 32-query wave units
+    int nw = tune_knob("DQ_WAVES", 0);
+    if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), D <= 64 ? 8 : 4, D <= 64 ? 2 : 4);
     if constexpr (D <= 64) {
-        if (tune_knob("DQ_WAVES", 8) == 8) return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        if (nw == 8) return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        if (nw == 2) return dq_launch<D, 2>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
     }
     return dq_launch<D, 4>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
 }

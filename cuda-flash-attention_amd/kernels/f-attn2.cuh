@@ -90,4 +90,10 @@ inline bool supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 // measured best and what ships.
 int tune_knob(const char* name, int dflt);
 
+// Waves per workgroup for a grid of `blocks32` 32-row wave units: the largest of
+// maxnw, maxnw/2, ..., minnw whose grid still covers every CU of the current device
+// (small problems get smaller workgroups, more of them, and waves with their SIMD
+// to themselves); maxnw when even that grid fills the chip.
+int auto_waves(long blocks32, int maxnw, int minnw = 2);
+
 }  // namespace fa2

@@ -731,9 +731,13 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     // ~400 VGPRs (8 would spill and exceed the LDS budget with the Q stages)
     // (MQ = 2, two 32-row query groups per wave at 4 waves / 1 per SIMD, measured
     // 30 % slower than 8 waves x 1 group at D = 32 and 64 -- r01)
+    // FA2_TUNE_FWD_WAVES = 0 (default): auto_waves over the grid of 32-query wave units
+    int nw = tune_knob("FWD_WAVES", 0);
+    if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), D <= 64 ? 8 : 4);
     if constexpr (D <= 64) {
-        if (tune_knob("FWD_WAVES", 8) == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
+        if (nw == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
     }
+    if (nw == 2) return fwd_f16_launch<D, 2>(q, k, v, o, lse, bh, S, stream);
     return fwd_f16_launch<D, 4>(q, k, v, o, lse, bh, S, stream);
 }
 
