@@ -229,22 +229,24 @@ __device__ __forceinline__ f32x16 splat16(float x) {
 
 // S^T of one 64-key tile for the wave's MQ query groups (keys on registers, query
 // on the lane), relative to m.  Each K fragment read from LDS feeds MQ MFMAs.
-template <int D, int MQ, int ABL = 0>
-__device__ __forceinline__ void fwd_qk(f32x16 (&s)[MQ][2], const FwdState<D> (&st)[MQ], const _Float16* Ks,
+// SEED: the chain starts from -m (scores relative to m); otherwise from 0 and the
+// softmax subtracts m per score (32-key tiles at D = 128, 16 registers fewer).
+template <int D, int MQ, int ABL = 0, int NKB = 2, bool SEED = true>
+__device__ __forceinline__ void fwd_qk(f32x16 (&s)[MQ][NKB], const FwdState<D> (&st)[MQ], const _Float16* Ks,
                                        const FragOffsets<D>& fo) {
     if (ABL & 16) {
 #pragma unroll
-        for (int g = 0; g < MQ; ++g) {
-            s[g][0] = st[g].nm + fo.rowop(Ks, 0, 0)[0];
-            s[g][1] = st[g].nm;
-        }
+        for (int g = 0; g < MQ; ++g)
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) s[g][kb] = st[g].nm + fo.rowop(Ks, 0, 0)[kb];
         return;
     }
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int kb = 0; kb < NKB; ++kb) {
         const f16x8 a0 = fo.rowop(Ks, kb * 32, 0);
+        const f32x16 zero = {};
 #pragma unroll
-        for (int g = 0; g < MQ; ++g) s[g][kb] = mfma(a0, st[g].qf[0], st[g].nm);
+        for (int g = 0; g < MQ; ++g) s[g][kb] = mfma(a0, st[g].qf[0], SEED ? st[g].nm : zero);
 #pragma unroll
         for (int t = 1; t < D / 16; ++t) {
             const f16x8 a = fo.rowop(Ks, kb * 32, t);
@@ -254,26 +256,30 @@ __device__ __forceinline__ void fwd_qk(f32x16 (&s)[MQ][2], const FwdState<D> (&s
     }
 }
 
-// Row max of a 32-score register tile as four independent max3 chains.
-__device__ __forceinline__ float tile_max(const f32x16 (&t)[2]) {
+// Row max of a 16*NKB-score register tile as four independent max3 chains.
+template <int NKB>
+__device__ __forceinline__ float tile_max(const f32x16 (&t)[NKB]) {
     float c[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         c[k] = fmaxf(t[0][k], t[0][k + 4]);
         c[k] = fmaxf(fmaxf(c[k], t[0][k + 8]), t[0][k + 12]);
-        c[k] = fmaxf(fmaxf(c[k], t[1][k]), t[1][k + 4]);
-        c[k] = fmaxf(fmaxf(c[k], t[1][k + 8]), t[1][k + 12]);
+#pragma unroll
+        for (int kb = 1; kb < NKB; ++kb) {
+            c[k] = fmaxf(fmaxf(c[k], t[kb][k]), t[kb][k + 4]);
+            c[k] = fmaxf(fmaxf(c[k], t[kb][k + 8]), t[kb][k + 12]);
+        }
     }
     return fmaxf(fmaxf(c[0], c[1]), fmaxf(c[2], c[3]));
 }
 
 // p = exp2(s - m - sh) of the tile, packed to fp16, with its four partial row sums.
-template <bool SHIFT, int ABL = 0>
-__device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[2], float sh, f16x8 (&pf)[2][2], float (&ls)[4]) {
+template <bool SHIFT, int ABL = 0, int NKB = 2>
+__device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[NKB], float sh, f16x8 (&pf)[NKB][2], float (&ls)[4]) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) ls[c] = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const float x = SHIFT ? sacc[kb][i] - sh : sacc[kb][i];
@@ -287,26 +293,26 @@ __device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[2], float sh, f16x8
 // O^T += V^T P^T with the packed scores as the B operand (each V^T fragment feeds MQ
 // MFMAs).  first: the wave's first tile (m := its row max).  One slow-path decision
 // for all groups keeps the tile a single basic block on the common path.
-template <int D, int MQ, bool MASK, int ABL = 0>
-__device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&sacc)[MQ][2], const _Float16* Vs,
+template <int D, int MQ, bool MASK, int ABL = 0, int NKB = 2, bool SEED = true>
+__device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&sacc)[MQ][NKB], const _Float16* Vs,
                                                const FragOffsets<D>& fo, int k0, int S, int h, bool first) {
     if (MASK) {  // ragged last tile only
 #pragma unroll
         for (int g = 0; g < MQ; ++g)
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
+            for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
                 for (int i = 0; i < 16; ++i)
                     if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sacc[g][kb][i] = -__builtin_inff();
     }
-    f16x8 pf[MQ][2][2];
+    f16x8 pf[MQ][NKB][2];
     float ls[MQ][4];
     bool slow = first;
     if (!first) {
         bool bad = false;
 #pragma unroll
         for (int g = 0; g < MQ; ++g) {
-            fwd_exp<false, ABL>(sacc[g], 0.f, pf[g], ls[g]);
+            fwd_exp<!SEED, ABL, NKB>(sacc[g], st[g].m, pf[g], ls[g]);
             const float ts = (ls[g][0] + ls[g][1]) + (ls[g][2] + ls[g][3]);
             bad = bad || !(ts <= FA2_TILE_SUM_MAX);
         }
@@ -315,7 +321,7 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
     if (slow) {
 #pragma unroll
         for (int g = 0; g < MQ; ++g) {
-            const float mx = xor32_max(tile_max(sacc[g]));
+            const float mx = xor32_max(tile_max<NKB>(sacc[g])) - (SEED ? 0.f : st[g].m);
             const float d = first ? mx : fmaxf(mx, 0.f);
             const float alpha = first ? 0.f : fast_exp2(-d);
             st[g].m += d;
@@ -325,8 +331,8 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
             for (int b = 0; b < D / 32; ++b)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) st[g].oacc[b][i] *= alpha;
-            st[g].nm = splat16(-st[g].m);
-            fwd_exp<true, ABL>(sacc[g], d, pf[g], ls[g]);
+            if (SEED) st[g].nm = splat16(-st[g].m);
+            fwd_exp<true, ABL, NKB>(sacc[g], SEED ? d : st[g].m, pf[g], ls[g]);
         }
     }
 #pragma unroll
@@ -336,7 +342,7 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const f16x8 v = fo.trop(Vs, kb * 32 + 16 * s, b);
@@ -348,7 +354,7 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
             }
 }
 
-template <int D>
+template <int D, bool SEED = true>
 __device__ __forceinline__ void fwd_init(FwdState<D>& st, const float* Q, long base, int q, int S, int h) {
     const float qscale = FA2_LOG2E / __builtin_sqrtf((float)D);
     // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16t + 8h + 0..7]
@@ -365,7 +371,7 @@ __device__ __forceinline__ void fwd_init(FwdState<D>& st, const float* Q, long b
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
         for (int i = 0; i < 16; ++i) st.oacc[b][i] = 0.f;
-    st.nm = splat16(0.f);
+    if (SEED) st.nm = splat16(0.f);
     st.m = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) st.l[c] = 0.f;
@@ -435,15 +441,20 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 
 // MQ 32-row query groups per wave (MQ = 2: two independent MFMA / softmax chains
 // per wave for the scheduler to interleave, each K / V^T fragment feeding two MFMAs).
-template <int D, int NW, int MQ, int ABL = 0>
+// NKB 32-key blocks per KV tile (2: 64-key tiles; 1: 32-key tiles, fewer registers
+// for D = 128 at 8 waves).
+template <int D, int NW, int MQ, int ABL = 0, int NKB = 2>
 __global__ void __launch_bounds__(64 * NW)
 fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                    float* __restrict__ O, float* __restrict__ LSE, int S FA2_STAMP_ARG) {
-    constexpr int KT = 64;  // keys per tile
+    constexpr bool SEED = NKB == 2;  // -m seed for 64-key tiles; 32-key tiles subtract m
+    constexpr int KT = 32 * NKB;  // keys per tile
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
     constexpr int QW = 32 * MQ;  // query rows per wave
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];  // [buf][K | V]
+    // [buf][K | V] tiles; at least one Q block (coalesced prologue) in size
+    constexpr int SMEM = (4 * TILE > 32 * MQ * NW * D) ? 4 * TILE : 32 * MQ * NW * D;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
 #if FA2_FWD_COAL
     __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];  // per-wave O block stage
 #endif
@@ -462,7 +473,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     // Q block (32*MQ*NW rows, one contiguous HBM range) loaded row-coalesced, converted
     // and scaled into the (still idle) K/V LDS buffers, then read back as this wave's
     // B fragments: 1 KB per load instruction instead of 32 rows x 32 B per-lane pieces.
-    static_assert(32 * MQ * NW <= 4 * KT, "Q block fits the K/V buffers");
     {
         TileStager<D, 32 * MQ * NW, NT> qst;
         qst.init(Q + base, S, tid);
@@ -471,7 +481,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         __syncthreads();
 #pragma unroll
         for (int g = 0; g < MQ; ++g) {
-            fwd_init<D>(st[g], nullptr, 0, S, S, h);  // state only (q >= S: no Q read)
+            fwd_init<D, SEED>(st[g], nullptr, 0, S, S, h);  // state only (q >= S: no Q read)
 #pragma unroll
             for (int t = 0; t < D / 16; ++t) st[g].qf[t] = fo.rowop(smem, wave * QW + 32 * g, t);
         }
@@ -479,7 +489,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     }
 #else
 #pragma unroll
-    for (int g = 0; g < MQ; ++g) fwd_init<D>(st[g], Q, base, q0 + 32 * g, S, h);
+    for (int g = 0; g < MQ; ++g) fwd_init<D, SEED>(st[g], Q, base, q0 + 32 * g, S, h);
 #endif
     // K/V staging by the first FA2_FWD_SW waves (all when 0): the second half loses
     // VALU arbitration to its SIMD partners, so the first half takes the staging
@@ -509,15 +519,16 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                 vs.load((j + 1) * KT);
             }
             FA2_STAMP(0);
-            f32x16 sacc[MQ][2];
-            fwd_qk<D, MQ, ABL>(sacc, st, smem, fo);
+            f32x16 sacc[MQ][NKB];
+            fwd_qk<D, MQ, ABL, NKB, SEED>(sacc, st, smem, fo);
             if (more && FA2_FWD_LP) {
                 ks.load((j + 1) * KT);
                 vs.load((j + 1) * KT);
             }
             FA2_STAMP(1);
-            if (j == last_ragged) fwd_softmax_pv<D, MQ, true, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
-            else fwd_softmax_pv<D, MQ, false, ABL>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
+            if (j == last_ragged)
+                fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
+            else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
             FA2_STAMP(2);
             if (more) {
                 ks.store(smem + 2 * TILE, 1.f, tid);
@@ -534,16 +545,16 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                 vs.load((j + 2) * KT);
             }
             FA2_STAMP(0);
-            f32x16 sacc[MQ][2];
-            fwd_qk<D, MQ, ABL>(sacc, st, smem + 2 * TILE, fo);
+            f32x16 sacc[MQ][NKB];
+            fwd_qk<D, MQ, ABL, NKB, SEED>(sacc, st, smem + 2 * TILE, fo);
             if (more && FA2_FWD_LP) {
                 ks.load((j + 2) * KT);
                 vs.load((j + 2) * KT);
             }
             FA2_STAMP(1);
             if (j + 1 == last_ragged)
-                fwd_softmax_pv<D, MQ, true, ABL>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
-            else fwd_softmax_pv<D, MQ, false, ABL>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+                fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+            else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
             FA2_STAMP(2);
             if (more) {
                 ks.store(smem, 1.f, tid);
@@ -679,7 +690,7 @@ struct StampLog {
 static StampLog g_stamps;
 #endif
 
-template <int D, int NW, int MQ, int ABL>
+template <int D, int NW, int MQ, int ABL, int NKB = 2>
 static void fwd_f16_go(const float* q, const float* k, const float* v, float* o, float* lse, long grid, int S,
                        hipStream_t stream) {
 #ifdef FA2_STAMPS
@@ -691,7 +702,7 @@ static void fwd_f16_go(const float* q, const float* k, const float* v, float* o,
         (void)hipMalloc(&buf, n * sizeof(unsigned long long));
         cap = n;
     }
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, MQ, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, MQ, ABL, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
                        v, o, lse, S, buf);
     std::vector<unsigned long long> h(n);
     (void)hipStreamSynchronize(stream);
@@ -699,12 +710,12 @@ static void fwd_f16_go(const float* q, const float* k, const float* v, float* o,
     for (long i = 0; i < n; ++i) g_stamps.sum[i % FA2_NSTAMP] += (double)h[i] / (grid * NW);
     ++g_stamps.launches;
 #else
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, MQ, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, MQ, ABL, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
                        v, o, lse, S);
 #endif
 }
 
-template <int D, int NW, int MQ = 1>
+template <int D, int NW, int MQ = 1, int NKB = 2>
 static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
                                  hipStream_t stream) {
     const int nqb = (S + 32 * MQ * NW - 1) / (32 * MQ * NW);
@@ -720,7 +731,7 @@ static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v,
         default: break;
     }
 #endif
-    fwd_f16_go<D, NW, MQ, 0>(q, k, v, o, lse, grid, S, stream);
+    fwd_f16_go<D, NW, MQ, 0, NKB>(q, k, v, o, lse, grid, S, stream);
     return hipGetLastError();
 }
 
@@ -733,9 +744,12 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     // 30 % slower than 8 waves x 1 group at D = 32 and 64 -- r01)
     // FA2_TUNE_FWD_WAVES = 0 (default): auto_waves over the grid of 32-query wave units
     int nw = tune_knob("FWD_WAVES", 0);
-    if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), D <= 64 ? 8 : 4);
+    if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), 8);
     if constexpr (D <= 64) {
         if (nw == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
+    } else {
+        // D = 128 at 8 waves only with 32-key tiles (64-key tiles spill)
+        if (nw == 8) return fwd_f16_launch<D, 8, 1, 1>(q, k, v, o, lse, bh, S, stream);
     }
     if (nw == 2) return fwd_f16_launch<D, 2>(q, k, v, o, lse, bh, S, stream);
     return fwd_f16_launch<D, 4>(q, k, v, o, lse, bh, S, stream);
