@@ -579,15 +579,15 @@ struct DqState {
     f32x16 nlse2, ndel;            // loop-invariant initial accumulators: -lse2, -delta (per lane)
 };
 
-// One 64-key tile: S^T = K Q^T and dP^T = V dO^T with the query on the lane,
+// One (32*NKB)-key tile: S^T = K Q^T and dP^T = V dO^T with the query on the lane,
 // dS^T = P^T*(dP^T - Delta), dQ^T += K^T dS^T (K^T through ds_read_b64_tr_b16).
-template <int D, bool MASK, typename Mid>
+template <int D, bool MASK, int NKB, typename Mid>
 __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, const _Float16* Vs,
                                         const FragOffsets<D>& fo, int k0, int S, int h, Mid&& mid) {
-    f16x8 dsf[2][2];
+    f16x8 dsf[NKB][2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-        if (kb == 1) mid();  // between the two key blocks (next tile's loads, FA2_DQ_LP)
+    for (int kb = 0; kb < NKB; ++kb) {
+        if (NKB > 1 && kb == 1) mid();  // between the two key blocks (next tile's loads, FA2_DQ_LP)
         // rows: key k0 + kb*32 + (i&3) + 8*(i>>2) + 4h ; col: query (lane)
         f32x16 sa = st.nlse2, da = st.ndel;
 #pragma unroll
@@ -595,6 +595,7 @@ __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, cons
             sa = mfma(fo.rowop(Ks, kb * 32, t), st.qf[t], sa);
             da = mfma(fo.rowop(Vs, kb * 32, t), st.df[t], da);
         }
+        if (NKB == 1) mid();  // after the tile's S / dP MFMAs
         if (MASK) {  // ragged last tile only
 #pragma unroll
             for (int i = 0; i < 16; ++i)
@@ -606,22 +607,25 @@ __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, cons
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
             for (int s = 0; s < 2; ++s) st.dqa[b] = mfma(fo.trop(Ks, kb * 32 + 16 * s, b), dsf[kb][s], st.dqa[b]);
 }
 
 // DELTA: Δ is computed here (from O, fused into the dO prologue) and written to
 // `Delta` for the dK/dV kernel, which then runs after this one.
-template <int D, int NW, bool DELTA = false>
+// NKB 32-key blocks per K/V tile (1 for D = 128 at 8 waves: fewer registers).
+template <int D, int NW, bool DELTA = false, int NKB = 2>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                       const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
                       float* __restrict__ dQ, int S, const float* __restrict__ O) {
-    constexpr int KT = 64;
+    constexpr int KT = 32 * NKB;
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
+    // [buf][K | V] tiles; at least one Q block (coalesced prologue) in size
+    constexpr int SMEM = (4 * TILE > 32 * NW * D) ? 4 * TILE : 32 * NW * D;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
 #if FA2_BWD_COAL
     __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];  // per-wave dQ stage
 #endif
@@ -639,7 +643,6 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     FragOffsets<D> fo;
     fo.init(lane);
 #if FA2_BWD_COAL
-    static_assert(32 * NW <= 4 * KT, "Q / dO block fits the K/V buffers");
     stage_block<D, 32 * NW, NT>(smem, Q + base, S, qb * 32 * NW, qscale, tid);
     __syncthreads();
 #pragma unroll
@@ -704,8 +707,8 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
             auto mid = [&] {
                 if (more && FA2_DQ_LP) ld();
             };
-            if (j == last_ragged) dq_tile<D, true>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
-            else dq_tile<D, false>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
+            if (j == last_ragged) dq_tile<D, true, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
+            else dq_tile<D, false, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
             if (more) {
                 ks.store(smem + 2 * TILE, 1.f, tid);
                 vs.store(smem + 3 * TILE, 1.f, tid);
@@ -723,8 +726,8 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
                 if (more && FA2_DQ_LP) ld();
             };
             if (j + 1 == last_ragged)
-                dq_tile<D, true>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
-            else dq_tile<D, false>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
+                dq_tile<D, true, NKB>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
+            else dq_tile<D, false, NKB>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
             if (more) {
                 ks.store(smem, 1.f, tid);
                 vs.store(smem + TILE, 1.f, tid);
@@ -1015,18 +1018,18 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     if (nw == 2) return dkdv_launch<D, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
-template <int D, int NW>
+template <int D, int NW, int NKB = 2>
 hipError_t dq_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                      float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
     const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
 #if FA2_BWD_COAL
     if (o)
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true>), dim3((unsigned)grid), dim3(64 * NW), 0,
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0,
                            stream, q, k, v, dout, lse, delta, dq, S, o);
     else
 #endif
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false>), dim3((unsigned)grid), dim3(64 * NW), 0,
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0,
                            stream, q, k, v, dout, lse, delta, dq, S, o);
     return hipGetLastError();
 }
@@ -1036,6 +1039,8 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     // 8 waves (2 per SIMD) for D <= 64; at D = 128 8 waves spill (~120 VGPRs), so 4
     // FA2_TUNE_DQ_WAVES = 0 (default): auto_waves over the grid of 32-query wave units
     int nw = tune_knob("DQ_WAVES", 0);
+    // (D = 128 at 8 waves spills even with 32-key tiles: Q, dO fragments, the -LSE / -Δ
+    // seeds and the dQ accumulators alone are 160 VGPRs -- r01)
     if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), D <= 64 ? 8 : 4, D <= 64 ? 2 : 4);
     if constexpr (D <= 64) {
         if (nw == 8) return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
