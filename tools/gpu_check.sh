@@ -22,7 +22,7 @@ for s in $STEPS; do
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider ${PYTEST_ARGS} ;;
     bench)  run bench 600 python bench.py ${BENCH_ARGS} ;;
-    prof)   run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extras --steps 10 --warmup 3 ;;
+    prof)   run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extras --steps 50 --warmup 20 ;;
   esac
 done
 echo done >> $OUT/status.txt

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", action="append", default=[], help="alternate libfa2amd.so builds to A/B (repeatable)")
+    ap.add_argument("--do", choices=["randn", "ones"], default="randn", help="dO distribution (bench.py uses ones)")
     args = ap.parse_args()
     import torch
     import fa2amd
@@ -31,7 +32,7 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(42)
     q, k, v = (torch.rand(B, H, S, D, generator=g).to(dev) for _ in range(3))
-    do = torch.randn(B, H, S, D, generator=g).to(dev)
+    do = torch.randn(B, H, S, D, generator=g).to(dev) if args.do == "randn" else torch.ones(B, H, S, D, device=dev)
     o, lse = fa2amd.forward(q, k, v, "fp16")
     dl = fa2amd.delta(do, o)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
