@@ -307,6 +307,29 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
     }
     f16x8 pf[MQ][NKB][2];
     float ls[MQ][4];
+    // l += tile sums, O^T += V^T P^T.  Issued inside each branch (64-key tiles): joining
+    // the paths before it made the register allocator copy O and l (29 v_mov per tile
+    // on the common path, r01 ISA audit); joined after it, the merged values are MFMA
+    // results.  32-key tiles (D = 128 at 8 waves) join first: the duplicate spills.
+    auto accumulate = [&]() {
+#pragma unroll
+        for (int g = 0; g < MQ; ++g)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) st[g].l[c] += ls[g][c];
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const f16x8 v = fo.trop(Vs, kb * 32 + 16 * s, b);
+#pragma unroll
+                    for (int g = 0; g < MQ; ++g) {
+                        if (ABL & 8) st[g].oacc[b][s + 2 * kb] += (float)pf[g][kb][s][b] + (float)v[0];
+                        else st[g].oacc[b] = mfma(v, pf[g][kb][s], st[g].oacc[b]);
+                    }
+                }
+    };
     bool slow = first;
     if (!first) {
         bool bad = false;
@@ -334,24 +357,11 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
             if (SEED) st[g].nm = splat16(-st[g].m);
             fwd_exp<true, ABL, NKB>(sacc[g], SEED ? d : st[g].m, pf[g], ls[g]);
         }
+        if (NKB == 2) accumulate();
+    } else if (NKB == 2) {
+        accumulate();
     }
-#pragma unroll
-    for (int g = 0; g < MQ; ++g)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) st[g].l[c] += ls[g][c];
-#pragma unroll
-    for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const f16x8 v = fo.trop(Vs, kb * 32 + 16 * s, b);
-#pragma unroll
-                for (int g = 0; g < MQ; ++g) {
-                    if (ABL & 8) st[g].oacc[b][s + 2 * kb] += (float)pf[g][kb][s][b] + (float)v[0];
-                    else st[g].oacc[b] = mfma(v, pf[g][kb][s], st[g].oacc[b]);
-                }
-            }
+    if (NKB != 2) accumulate();
 }
 
 template <int D, bool SEED = true>
