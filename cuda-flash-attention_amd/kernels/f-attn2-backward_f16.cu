@@ -341,6 +341,14 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
 #ifndef FA2_DKDV_SW
 #define FA2_DKDV_SW 4
 #endif
+// FA2_*_PRIO: s_setprio 1 for waves 4-7 of 8-wave workgroups (the second-dispatched
+// half loses VALU arbitration by age; MI355X_MICROARCH §Two waves per SIMD, item 4)
+#ifndef FA2_DKDV_PRIO
+#define FA2_DKDV_PRIO 0
+#endif
+#ifndef FA2_DQ_PRIO
+#define FA2_DQ_PRIO 1
+#endif
 #ifndef FA2_DQ_SW
 #define FA2_DQ_SW 0
 #endif
@@ -453,6 +461,7 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     // compiler drain vmcnt -- the K/V staging loads too -- at every step start).
     static_assert(QT == 64, "one wave per row vector");
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    if (FA2_DKDV_PRIO && NW == 8 && wave_u >= NW / 2) __builtin_amdgcn_s_setprio(1);
     const __amdgpu_buffer_rsrc_t rs_lse = head_rsrc(LSE + rbase, S, 1);
     const __amdgpu_buffer_rsrc_t rs_del = head_rsrc(Delta + rbase, S, 1);
     float rowraw = 0.f;
@@ -688,6 +697,7 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
     ks.on = vs.on = __builtin_amdgcn_readfirstlane(wave) < SW;
+    if (FA2_DQ_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
     const int ntiles = (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     ks.load(0);

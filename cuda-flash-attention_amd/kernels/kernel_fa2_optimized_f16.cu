@@ -449,12 +449,84 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 #define FA2_STAMP_ARG
 #endif
 
+// FA2_FWD_STAG (8-wave workgroups): waves 4-7 run half a tile behind waves 0-3.
+// The two waves of a SIMD (w, w + 4) run the same program, and the per-tile barrier
+// kept them in lockstep: both in QK^T (MFMA) together, then both in the softmax
+// (VALU) together.  Staggered, the lagging wave finishes tile j-1 (softmax + PV)
+// while its partner computes QK^T of tile j, and runs its own QK^T of tile j while
+// the partner is in the softmax (guide MI355X_MICROARCH §Two waves per SIMD, item 9).
+// V of tile j-1 is read one interval later, so the K/V ring has three slots.
+#ifndef FA2_FWD_STAG
+#define FA2_FWD_STAG 0
+#endif
+// FA2_FWD_PRIO: s_setprio 1 for waves 4-7 of an 8-wave workgroup for the whole loop
+// (the second-dispatched half loses VALU arbitration by age; guide item 4)
+#ifndef FA2_FWD_PRIO
+#define FA2_FWD_PRIO 1
+#endif
+// FA2_FWD_W4_OCC: waves per SIMD the 4-wave kernel is register-budgeted for (2: two
+// independent 4-wave workgroups per CU, whose SIMD partners share no barrier)
+#ifndef FA2_FWD_W4_OCC
+#define FA2_FWD_W4_OCC 1
+#endif
+
+template <int N>
+struct Slot {
+    static constexpr int value = N;
+};
+
+// The tile loop of a staggered workgroup: ONE body for both halves (one register
+// allocation), iteration i = { load tile i+1; softmax + PV of tile i-1; QK^T of
+// tile i; store tile i+1 }, with the barrier placed per half:
+//   leading half (waves 0..NW/2-1): before QK^T (from i = 1), and once after the
+//     final softmax -> interval k holds its QK^T(k-1), softmax(k-1);
+//   lagging half: after the store -> interval k holds its softmax(k-2), QK^T(k-1).
+// Both halves store tile k in interval k into slot k % 3 while the workgroup reads
+// slots (k-1) % 3 and (k-2) % 3 only.  S^T of tile i is carried into iteration
+// i+1; QK^T of tile i always follows the softmax of tile i-1 (it reads -m), so the
+// arithmetic, and the outputs, are those of the unstaggered loop.
+template <int D, int MQ, int ABL, int NKB, bool SEED, class Stager>
+__device__ __forceinline__ void fwd_loop_stag(FwdState<D> (&st)[MQ], _Float16* smem, const FragOffsets<D>& fo,
+                                              Stager& ks, Stager& vs, int ntiles, int last_ragged, int S, int h,
+                                              int tid, bool lead) {
+    constexpr int KT = 32 * NKB;
+    constexpr int TILE = KT * D;
+    f32x16 sprev[MQ][NKB];
+    auto softmax = [&](const _Float16* Vs, int j) {
+        if (j == last_ragged) fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sprev, Vs, fo, j * KT, S, h, j == 0);
+        else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sprev, Vs, fo, j * KT, S, h, j == 0);
+    };
+    auto step = [&](auto slot, int i) {
+        constexpr int sc = decltype(slot)::value, sp = (sc + 2) % 3, sn = (sc + 1) % 3;
+        const bool more = !(ABL & 1) && i + 1 < ntiles;
+        if (more) {
+            ks.load((i + 1) * KT);
+            vs.load((i + 1) * KT);
+        }
+        if (i > 0) softmax(smem + (2 * sp + 1) * TILE, i - 1);
+        if (lead && i > 0 && !(ABL & 4)) __syncthreads();
+        fwd_qk<D, MQ, ABL, NKB, SEED>(sprev, st, smem + 2 * sc * TILE, fo);
+        if (more) {
+            ks.store(smem + 2 * sn * TILE, 1.f, tid);
+            vs.store(smem + (2 * sn + 1) * TILE, 1.f, tid);
+        }
+        if (!lead && !(ABL & 4)) __syncthreads();
+    };
+    for (int i = 0; i < ntiles; i += 3) {
+        step(Slot<0>{}, i);
+        if (i + 1 < ntiles) step(Slot<1>{}, i + 1);
+        if (i + 2 < ntiles) step(Slot<2>{}, i + 2);
+    }
+    softmax(smem + (2 * ((ntiles - 1) % 3) + 1) * TILE, ntiles - 1);
+    if (lead && !(ABL & 4)) __syncthreads();
+}
+
 // MQ 32-row query groups per wave (MQ = 2: two independent MFMA / softmax chains
 // per wave for the scheduler to interleave, each K / V^T fragment feeding two MFMAs).
 // NKB 32-key blocks per KV tile (2: 64-key tiles; 1: 32-key tiles, fewer registers
 // for D = 128 at 8 waves).
 template <int D, int NW, int MQ, int ABL = 0, int NKB = 2>
-__global__ void __launch_bounds__(64 * NW)
+__global__ void __launch_bounds__(64 * NW, (NW == 4 && D <= 64) ? FA2_FWD_W4_OCC : 1)
 fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                    float* __restrict__ O, float* __restrict__ LSE, int S FA2_STAMP_ARG) {
     constexpr bool SEED = NKB == 2;  // -m seed for 64-key tiles; 32-key tiles subtract m
@@ -462,8 +534,10 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
     constexpr int QW = 32 * MQ;  // query rows per wave
-    // [buf][K | V] tiles; at least one Q block (coalesced prologue) in size
-    constexpr int SMEM = (4 * TILE > 32 * MQ * NW * D) ? 4 * TILE : 32 * MQ * NW * D;
+    constexpr bool STAG = FA2_FWD_STAG && NW == 8 && NKB == 2;
+    constexpr int NSLOT = STAG ? 3 : 2;
+    // [slot][K | V] tiles; at least one Q block (coalesced prologue) in size
+    constexpr int SMEM = (2 * NSLOT * TILE > 32 * MQ * NW * D) ? 2 * NSLOT * TILE : 32 * MQ * NW * D;
     __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
 #if FA2_FWD_COAL
     __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];  // per-wave O block stage
@@ -516,6 +590,11 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     vs.store(smem + TILE, 1.f, tid);
     __syncthreads();
 
+    if (FA2_FWD_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    if constexpr (STAG) {
+        fwd_loop_stag<D, MQ, ABL, NKB, SEED>(st, smem, fo, ks, vs, ntiles, last_ragged, S, h, tid,
+                                             __builtin_amdgcn_readfirstlane(wave) < NW / 2);
+    } else {
 #ifdef FA2_STAMPS
     unsigned long long stv[FA2_NSTAMP] = {0, 0, 0, 0, 0}, tprev;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
@@ -579,6 +658,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     if (lane == 0)
         for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blockIdx.x * NW + wave) * FA2_NSTAMP + k] = stv[k];
 #endif
+    }
 #if FA2_FWD_COAL
     // O through a wave-private LDS stage, one 32x32 block at a time, stored as whole
     // 128-B row segments (8 rows per instruction) instead of 16-B pieces of 32 rows
