@@ -159,6 +159,9 @@ def extras(fa2amd, torch, dev):
     out["c4_B8_H16_S4096_D128_fp16_fwd"] = {"ms": round(ms, 4), "tflops": round(tf, 2), "hbm_gbps": round(gbps, 1),
                                             "frac_mfma": round(tf / MFMA_F16_PEAK_TFLOPS, 4),
                                             "frac_hbm": round(gbps / HBM_PEAK_GBPS, 4)}
+    ms, tf, gbps = time_config(fa2amd, torch, dev, 4, 16, 2048, 64, "bf16", False)
+    out["c3_B4_H16_S2048_D64_bf16_fwdbwd"] = {"ms": round(ms, 4), "tflops": round(tf, 2),
+                                              "frac_mfma": round(tf / MFMA_F16_PEAK_TFLOPS, 4)}
     ms, tf, gbps = time_config(fa2amd, torch, dev, 2, 8, 512, 64, "fp32", False)
     out["c2_B2_H8_S512_D64_fp32_fwdbwd"] = {"ms": round(ms, 4), "tflops": round(tf, 2),
                                             "frac_mfma_f32": round(tf / MFMA_F32_PEAK_TFLOPS, 4)}
@@ -174,7 +177,7 @@ def main():
                     help="keep warming (untimed) until at least this much wall time has passed: the "
                          "power-capped MI355X needs ~0.2 s of load to reach its steady clock")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
-    ap.add_argument("--precision", choices=["fp16", "fp32"], default="fp16")
+    ap.add_argument("--precision", choices=["fp16", "fp32", "bf16"], default="fp16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the S sweep / C2 / C4 extra configs")
     args = ap.parse_args()
@@ -287,7 +290,7 @@ def main():
     alg = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "delta": 0.0, "bwd": 10.0}
     dom = max(kms, key=kms.get)
     dom_flops = alg[dom] * per_head * heads
-    peak = MFMA_F16_PEAK_TFLOPS if prec == "fp16" else MFMA_F32_PEAK_TFLOPS
+    peak = MFMA_F16_PEAK_TFLOPS if prec in ("fp16", "bf16") else MFMA_F32_PEAK_TFLOPS
     achieved = dom_flops / (kms[dom] * 1e-3) / 1e12
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic_from_profile(dom, D, S, heads),

@@ -43,7 +43,8 @@ int hip_status(hipError_t e, const char* what) {
 }
 
 int check_precision(int precision) {
-    if (precision != FA2_FP16 && precision != FA2_FP32) return fail(FA2_E_INVALID, "precision must be FA2_FP16 or FA2_FP32");
+    if (precision != FA2_FP16 && precision != FA2_FP32 && precision != FA2_BF16)
+        return fail(FA2_E_INVALID, "precision must be FA2_FP16, FA2_FP32 or FA2_BF16");
     return FA2_OK;
 }
 
@@ -108,8 +109,9 @@ int fa2_forward(const float* q, const float* k, const float* v, float* o, float*
     if ((rc = check_shape(B, H, S, D)) || (rc = check_precision(precision)) || (rc = check_ptrs({q, k, v, o, lse})))
         return rc;
     const hipStream_t st = static_cast<hipStream_t>(stream);
-    const hipError_t e = precision == FA2_FP16 ? fa2::launch_forward_f16(D, q, k, v, o, lse, B * H, S, st)
-                                               : fa2::launch_forward_f32(D, q, k, v, o, lse, B * H, S, st);
+    const hipError_t e = precision == FA2_FP16   ? fa2::launch_forward_f16(D, q, k, v, o, lse, B * H, S, st)
+                         : precision == FA2_BF16 ? fa2::launch_forward_bf16(D, q, k, v, o, lse, B * H, S, st)
+                                                 : fa2::launch_forward_f32(D, q, k, v, o, lse, B * H, S, st);
     return hip_status(e, "fa2_forward launch");
 }
 
@@ -129,8 +131,9 @@ int fa2_backward(const float* q, const float* k, const float* v, const float* o,
         return rc;
     const hipStream_t st = static_cast<hipStream_t>(stream);
     const hipError_t e =
-        precision == FA2_FP16 ? fa2::launch_backward_f16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st)
-                              : fa2::launch_backward_f32(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st);
+        precision == FA2_FP16   ? fa2::launch_backward_f16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st)
+        : precision == FA2_BF16 ? fa2::launch_backward_bf16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st)
+                                : fa2::launch_backward_f32(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st);
     return hip_status(e, "fa2_backward launch");
 }
 

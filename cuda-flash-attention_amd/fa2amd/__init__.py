@@ -8,7 +8,9 @@ on a GPU, these functions raise -- there is no CPU fallback.
 Tensors are torch fp32, contiguous, [B, H, S, D] (logsumexp / delta [B, H, S]),
 exactly the reference's layout (detker/CUDA-Flash-Attention).
 ``precision`` is ``"fp16"`` (MFMA f16 tiles, fp32 accumulate -- the reference's
-``_f16.cu`` variants) or ``"fp32"`` (exact fp32 MFMA -- the reference's default).
+``_f16.cu`` variants), ``"fp32"`` (exact fp32 MFMA -- the reference's default) or
+``"bf16"`` (MFMA bf16 tiles, fp32 accumulate -- the reference README's "BF16
+precision support" improvement, README.md:504-508).
 """
 from __future__ import annotations
 
@@ -23,7 +25,9 @@ KERNEL_DIR = os.path.join(PKG_ROOT, "kernels")
 
 FA2_FP16 = 0
 FA2_FP32 = 1
-_PRECISION = {"fp16": FA2_FP16, "fp32": FA2_FP32, FA2_FP16: FA2_FP16, FA2_FP32: FA2_FP32}
+FA2_BF16 = 2
+_PRECISION = {"fp16": FA2_FP16, "fp32": FA2_FP32, "bf16": FA2_BF16,
+              FA2_FP16: FA2_FP16, FA2_FP32: FA2_FP32, FA2_BF16: FA2_BF16}
 SUPPORTED_HEAD_DIMS = (32, 64, 128)
 
 # exported symbols of include/fa2_amd.h (checked by tests/test_capi_symbols.py)

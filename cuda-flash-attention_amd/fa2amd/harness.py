@@ -73,16 +73,20 @@ class FA2Runner:
 class RawModuleRunner:
     """Drives kernels/kernel_fa2_optimized.cu and kernels/f-attn2-backward.cu exactly
     as test_flash_attention2.py does through cp.RawModule (the harness names the fp32
-    files only, :75-76; the _f16 files export the same symbols and can be passed)."""
+    files only, :75-76; the _f16 files export the same symbols and can be passed).
+    ``extra_options`` are appended to the harness's hiprtc options: the _f16 files
+    compiled with ``-DFA2_TILE_BF16`` run bf16 tiles behind the same symbols."""
 
     BLOCK_SIZE_R = 32
     BLOCK_SIZE_C = 32
 
-    def __init__(self, fwd_file="kernel_fa2_optimized.cu", bwd_file="f-attn2-backward.cu"):
-        from .rawmodule import RawModule, load_kernel_source
+    def __init__(self, fwd_file="kernel_fa2_optimized.cu", bwd_file="f-attn2-backward.cu", extra_options=()):
+        from .rawmodule import HARNESS_OPTIONS, RawModule, load_kernel_source
 
-        self.fwd_mod = RawModule(load_kernel_source(fwd_file), name_expressions=("flash_attention2_forward_kernel_wrapper",))
-        self.bwd_mod = RawModule(load_kernel_source(bwd_file), name_expressions=(
+        opts = tuple(HARNESS_OPTIONS) + tuple(extra_options)
+        self.fwd_mod = RawModule(load_kernel_source(fwd_file), options=opts,
+                                 name_expressions=("flash_attention2_forward_kernel_wrapper",))
+        self.bwd_mod = RawModule(load_kernel_source(bwd_file), options=opts, name_expressions=(
             "flash_attention2_backward_kernel_wrapper", "D_computation_reduction_kernel_wrapper"))
         self.fa2_kernel = self.fwd_mod.get_function("flash_attention2_forward_kernel_wrapper")
         self.backward_kernel = self.bwd_mod.get_function("flash_attention2_backward_kernel_wrapper")

@@ -32,6 +32,14 @@
 #endif
 #endif
 
+#ifdef FA2_TILE_BF16
+#define fa2f16b fa2bf16b
+#define FA2_TILE_LAUNCH(x) x##_bf16
+#define FA2_TILE_HOST(x) x##_bf16
+#else
+#define FA2_TILE_LAUNCH(x) x##_f16
+#define FA2_TILE_HOST(x) x##_fp16
+#endif
 namespace fa2f16b {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -43,9 +51,24 @@ typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 #define FA2B_LOG2E 1.4426950408889634f
 
+// Tile element type.  The default build stores fp16 tiles.  The same source compiled
+// with -DFA2_TILE_BF16 (Makefile: *_bf16.o, namespace fa2bf16b, launchers *_bf16)
+// keeps bf16 bits in the same 16-bit containers -- LDS images and fragments are only
+// moved (ds_read_b128 / ds_read_b64_tr_b16 are type-blind), never computed on,
+// except by the conversion below and the MFMA -- and runs the bf16 MFMA.
+#ifdef FA2_TILE_BF16
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ _Float16 to_tile(float x) { return __builtin_bit_cast(_Float16, (__bf16)x); }
+__device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+#else
+__device__ __forceinline__ _Float16 to_tile(float x) { return (_Float16)x; }
 __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
+#endif
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 template <int D> struct Swz;
@@ -76,8 +99,8 @@ __device__ __forceinline__ f16x8 cat4(i16x4 a, i16x4 b) {
 }
 __device__ __forceinline__ f16x8 to_f16x8(f32x4 a, f32x4 b, float s) {
     f16x8 r;
-    r[0] = (_Float16)(a[0] * s); r[1] = (_Float16)(a[1] * s); r[2] = (_Float16)(a[2] * s); r[3] = (_Float16)(a[3] * s);
-    r[4] = (_Float16)(b[0] * s); r[5] = (_Float16)(b[1] * s); r[6] = (_Float16)(b[2] * s); r[7] = (_Float16)(b[3] * s);
+    r[0] = to_tile(a[0] * s); r[1] = to_tile(a[1] * s); r[2] = to_tile(a[2] * s); r[3] = to_tile(a[3] * s);
+    r[4] = to_tile(b[0] * s); r[5] = to_tile(b[1] * s); r[6] = to_tile(b[2] * s); r[7] = to_tile(b[3] * s);
     return r;
 }
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -305,12 +328,12 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 if (ABL & 2) {
-                    pf[kb][i >> 3][i & 7] = (_Float16)sa[kb][i];
-                    dsf[kb][i >> 3][i & 7] = (_Float16)da[kb][i];
+                    pf[kb][i >> 3][i & 7] = to_tile(sa[kb][i]);
+                    dsf[kb][i >> 3][i & 7] = to_tile(da[kb][i]);
                 } else {
                     const float p = fast_exp2(sa[kb][i]);
-                    pf[kb][i >> 3][i & 7] = (_Float16)p;
-                    dsf[kb][i >> 3][i & 7] = (_Float16)(p * da[kb][i]);
+                    pf[kb][i >> 3][i & 7] = to_tile(p);
+                    dsf[kb][i >> 3][i & 7] = to_tile(p * da[kb][i]);
                 }
             }
         if (ABL & 8) {
@@ -611,7 +634,7 @@ __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, cons
                 if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) sa[i] = -__builtin_inff();
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dsf[kb][i >> 3][i & 7] = (_Float16)(fast_exp2(sa[i]) * da[i]);
+        for (int i = 0; i < 16; ++i) dsf[kb][i >> 3][i & 7] = to_tile(fast_exp2(sa[i]) * da[i]);
     }
 #pragma unroll
     for (int b = 0; b < D / 32; ++b)
@@ -863,9 +886,9 @@ __device__ __forceinline__ void bwd_compat_body(const float* __restrict__ Q, con
         for (int i = 0; i < 16; ++i) {
             const float p = kvalid ? fast_exp2(sa[i]) : 0.f;
             const float dsv = p * da[i];
-            pf[i >> 3][i & 7] = (_Float16)p;
-            dsf[i >> 3][i & 7] = (_Float16)dsv;
-            dsw[((i & 3) + 8 * (i >> 2) + 4 * h) * CompatLds::SLD + r] = (_Float16)dsv;
+            pf[i >> 3][i & 7] = to_tile(p);
+            dsf[i >> 3][i & 7] = to_tile(dsv);
+            dsw[((i & 3) + 8 * (i >> 2) + 4 * h) * CompatLds::SLD + r] = to_tile(dsv);
         }
         // dV^T += dO^T P
 #pragma unroll
@@ -1060,7 +1083,7 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
 }
 }  // namespace
 
-hipError_t launch_bwd_dkdv_f16(int D, const float* q, const float* k, const float* v, const float* dout,
+hipError_t FA2_TILE_LAUNCH(launch_bwd_dkdv)(int D, const float* q, const float* k, const float* v, const float* dout,
                                const float* lse, const float* delta, float* dk, float* dv, int bh, int S,
                                hipStream_t stream) {
     if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
@@ -1072,7 +1095,7 @@ hipError_t launch_bwd_dkdv_f16(int D, const float* q, const float* k, const floa
     }
 }
 
-hipError_t launch_bwd_dq_f16(int D, const float* q, const float* k, const float* v, const float* dout,
+hipError_t FA2_TILE_LAUNCH(launch_bwd_dq)(int D, const float* q, const float* k, const float* v, const float* dout,
                              const float* lse, const float* delta, float* dq, int bh, int S, hipStream_t stream) {
     if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
     float* dl = const_cast<float*>(delta);  // read only when o == nullptr
@@ -1084,7 +1107,7 @@ hipError_t launch_bwd_dq_f16(int D, const float* q, const float* k, const float*
     }
 }
 
-hipError_t launch_bwd_dq_delta_f16(int D, const float* q, const float* k, const float* v, const float* o,
+hipError_t FA2_TILE_LAUNCH(launch_bwd_dq_delta)(int D, const float* q, const float* k, const float* v, const float* o,
                                    const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
                                    hipStream_t stream) {
     if (bh <= 0 || S <= 0 || !o) return hipErrorInvalidValue;
@@ -1097,19 +1120,19 @@ hipError_t launch_bwd_dq_delta_f16(int D, const float* q, const float* k, const 
 }
 
 // Δ fused into the dQ kernel's prologue (which stages dO anyway); dK/dV reads it.
-hipError_t launch_backward_f16(int D, const float* q, const float* k, const float* v, const float* o,
+hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream) {
-    hipError_t e = launch_bwd_dq_delta_f16(D, q, k, v, o, dout, lse, delta, dq, bh, S, stream);
+    hipError_t e = FA2_TILE_LAUNCH(launch_bwd_dq_delta)(D, q, k, v, o, dout, lse, delta, dq, bh, S, stream);
     if (e != hipSuccess) return e;
-    return launch_bwd_dkdv_f16(D, q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+    return FA2_TILE_LAUNCH(launch_bwd_dkdv)(D, q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
 
 }  // namespace fa2
 
 // Host API with the reference's semantics (f-attn2-backward_f16.cu:375-474).
 template <int head_dim>
-void host_flash_attention2_backward_fp16(const float* h_Q, const float* h_K, const float* h_V, const float* h_O,
+void FA2_TILE_HOST(host_flash_attention2_backward)(const float* h_Q, const float* h_K, const float* h_V, const float* h_O,
                                          const float* h_dO, const float* h_lse, float* h_dQ, float* h_dK, float* h_dV,
                                          int batch_size, int seq_len, int num_heads, TimerManager* tm) {
     const size_t n = (size_t)batch_size * num_heads * seq_len * head_dim;
@@ -1120,7 +1143,7 @@ void host_flash_attention2_backward_fp16(const float* h_Q, const float* h_K, con
     const float* src[6] = {h_Q, h_K, h_V, h_O, h_dO, h_lse};
     for (int i = 0; i < 6; ++i) HIP_CHECK(hipMemcpy(d[i], src[i], sz[i] * sizeof(float), hipMemcpyHostToDevice));
     tm->Start();
-    HIP_CHECK(fa2::launch_backward_f16(head_dim, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9],
+    HIP_CHECK(fa2::FA2_TILE_LAUNCH(launch_backward)(head_dim, d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9],
                                        batch_size * num_heads, seq_len, nullptr));
     tm->Stop();
     HIP_CHECK(hipDeviceSynchronize());
@@ -1130,7 +1153,7 @@ void host_flash_attention2_backward_fp16(const float* h_Q, const float* h_K, con
     for (int i = 0; i < 10; ++i) HIP_CHECK(hipFree(d[i]));
 }
 #define FA2_INST_BWD16(D)                                                                                         \
-    template void host_flash_attention2_backward_fp16<D>(const float*, const float*, const float*, const float*, \
+    template void FA2_TILE_HOST(host_flash_attention2_backward)<D>(const float*, const float*, const float*, const float*, \
                                                          const float*, const float*, float*, float*, float*, int, \
                                                          int, int, TimerManager*);
 FA2_INST_BWD16(32)

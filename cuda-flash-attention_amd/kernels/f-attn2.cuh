@@ -49,6 +49,18 @@ void host_flash_attention2_backward_fp16(const float* query, const float* key, c
                                          float* deriv_query, float* deriv_key, float* deriv_value, int batch_size,
                                          int seq_len, int num_heads, TimerManager* tm);
 
+// bf16 tiles (the same kernels compiled with -DFA2_TILE_BF16; README "Possible
+// Improvements: BF16 precision support"), same semantics as the _fp16 templates
+template <int head_dim>
+void host_flash_attention2_forward_bf16(const float* h_Q, const float* h_K, const float* h_V, float* h_O,
+                                        float* h_logsumexp, int batch_size, int seq_len, int num_heads,
+                                        TimerManager* tm);
+template <int head_dim>
+void host_flash_attention2_backward_bf16(const float* query, const float* key, const float* value,
+                                         const float* output, const float* deriv_output, const float* logsumexp,
+                                         float* deriv_query, float* deriv_key, float* deriv_value, int batch_size,
+                                         int seq_len, int num_heads, TimerManager* tm);
+
 namespace fa2 {
 
 // Device-pointer launch layer.  All pointers are device memory, all launches are
@@ -82,6 +94,21 @@ hipError_t launch_bwd_dq_f16(int D, const float* q, const float* k, const float*
 hipError_t launch_bwd_dq_delta_f16(int D, const float* q, const float* k, const float* v, const float* o,
                                    const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
                                    hipStream_t stream);
+
+// bf16-tile twins of the *_f16 launchers above (kernels built from the same source)
+hipError_t launch_forward_bf16(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,
+                               int S, hipStream_t stream);
+hipError_t launch_backward_bf16(int D, const float* q, const float* k, const float* v, const float* o,
+                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
+                                int bh, int S, hipStream_t stream);
+hipError_t launch_bwd_dkdv_bf16(int D, const float* q, const float* k, const float* v, const float* dout,
+                                const float* lse, const float* delta, float* dk, float* dv, int bh, int S,
+                                hipStream_t stream);
+hipError_t launch_bwd_dq_bf16(int D, const float* q, const float* k, const float* v, const float* dout,
+                              const float* lse, const float* delta, float* dq, int bh, int S, hipStream_t stream);
+hipError_t launch_bwd_dq_delta_bf16(int D, const float* q, const float* k, const float* v, const float* o,
+                                    const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
+                                    hipStream_t stream);
 
 inline bool supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 

@@ -31,6 +31,14 @@
 #endif
 #endif
 
+#ifdef FA2_TILE_BF16
+#define fa2f16 fa2bf16
+#define FA2_TILE_LAUNCH(x) x##_bf16
+#define FA2_TILE_HOST(x) x##_bf16
+#else
+#define FA2_TILE_LAUNCH(x) x##_f16
+#define FA2_TILE_HOST(x) x##_fp16
+#endif
 namespace fa2f16 {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -43,9 +51,24 @@ typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 #define FA2_LOG2E 1.4426950408889634f
 #define FA2_LN2 0.6931471805599453f
 
+// Tile element type.  The default build stores fp16 tiles.  The same source compiled
+// with -DFA2_TILE_BF16 (Makefile: *_bf16.o, namespace fa2bf16, launchers *_bf16)
+// keeps bf16 bits in the same 16-bit containers -- LDS images and fragments are only
+// moved (ds_read_b128 / ds_read_b64_tr_b16 are type-blind), never computed on,
+// except by the conversion below and the MFMA -- and runs the bf16 MFMA.
+#ifdef FA2_TILE_BF16
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ _Float16 to_tile(float x) { return __builtin_bit_cast(_Float16, (__bf16)x); }
+__device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+#else
+__device__ __forceinline__ _Float16 to_tile(float x) { return (_Float16)x; }
 __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
+#endif
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -87,8 +110,8 @@ __device__ __forceinline__ f16x8 cat4(i16x4 a, i16x4 b) {
 
 __device__ __forceinline__ f16x8 to_f16x8(f32x4 a, f32x4 b, float s) {
     f16x8 r;
-    r[0] = (_Float16)(a[0] * s); r[1] = (_Float16)(a[1] * s); r[2] = (_Float16)(a[2] * s); r[3] = (_Float16)(a[3] * s);
-    r[4] = (_Float16)(b[0] * s); r[5] = (_Float16)(b[1] * s); r[6] = (_Float16)(b[2] * s); r[7] = (_Float16)(b[3] * s);
+    r[0] = to_tile(a[0] * s); r[1] = to_tile(a[1] * s); r[2] = to_tile(a[2] * s); r[3] = to_tile(a[3] * s);
+    r[4] = to_tile(b[0] * s); r[5] = to_tile(b[1] * s); r[6] = to_tile(b[2] * s); r[7] = to_tile(b[3] * s);
     return r;
 }
 
@@ -285,7 +308,7 @@ __device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[NKB], float sh, f16
             const float x = SHIFT ? sacc[kb][i] - sh : sacc[kb][i];
             const float p = (ABL & 2) ? x : fast_exp2(x);
             ls[i & 3] += p;
-            pf[kb][i >> 3][i & 7] = (_Float16)p;
+            pf[kb][i >> 3][i & 7] = to_tile(p);
         }
 }
 
@@ -845,7 +868,7 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     return fwd_f16_launch<D, 4>(q, k, v, o, lse, bh, S, stream);
 }
 
-hipError_t launch_forward_f16(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,
+hipError_t FA2_TILE_LAUNCH(launch_forward)(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,
                               int S, hipStream_t stream) {
     if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
     switch (D) {
@@ -861,7 +884,7 @@ hipError_t launch_forward_f16(int D, const float* q, const float* k, const float
 // Host API with the reference's semantics (kernel_fa2_optimized_f16.cu:353-430):
 // host buffers in, device alloc + H2D, timed launch, D2H, free.
 template <int head_dim>
-void host_flash_attention2_forward_fp16(const float* h_Q, const float* h_K, const float* h_V, float* h_O,
+void FA2_TILE_HOST(host_flash_attention2_forward)(const float* h_Q, const float* h_K, const float* h_V, float* h_O,
                                         float* h_logsumexp, int batch_size, int seq_len, int num_heads,
                                         TimerManager* tm) {
     const size_t n = (size_t)batch_size * num_heads * seq_len * head_dim;
@@ -876,7 +899,7 @@ void host_flash_attention2_forward_fp16(const float* h_Q, const float* h_K, cons
     HIP_CHECK(hipMemcpy(dk, h_K, n * sizeof(float), hipMemcpyHostToDevice));
     HIP_CHECK(hipMemcpy(dv, h_V, n * sizeof(float), hipMemcpyHostToDevice));
     tm->Start();
-    HIP_CHECK(fa2::launch_forward_f16(head_dim, dq, dk, dv, dout, dl, batch_size * num_heads, seq_len, nullptr));
+    HIP_CHECK(fa2::FA2_TILE_LAUNCH(launch_forward)(head_dim, dq, dk, dv, dout, dl, batch_size * num_heads, seq_len, nullptr));
     tm->Stop();
     HIP_CHECK(hipDeviceSynchronize());
     HIP_CHECK(hipMemcpy(h_O, dout, n * sizeof(float), hipMemcpyDeviceToHost));
@@ -887,11 +910,11 @@ void host_flash_attention2_forward_fp16(const float* h_Q, const float* h_K, cons
     HIP_CHECK(hipFree(dout));
     HIP_CHECK(hipFree(dl));
 }
-template void host_flash_attention2_forward_fp16<32>(const float*, const float*, const float*, float*, float*, int,
+template void FA2_TILE_HOST(host_flash_attention2_forward)<32>(const float*, const float*, const float*, float*, float*, int,
                                                      int, int, TimerManager*);
-template void host_flash_attention2_forward_fp16<64>(const float*, const float*, const float*, float*, float*, int,
+template void FA2_TILE_HOST(host_flash_attention2_forward)<64>(const float*, const float*, const float*, float*, float*, int,
                                                      int, int, TimerManager*);
-template void host_flash_attention2_forward_fp16<128>(const float*, const float*, const float*, float*, float*, int,
+template void FA2_TILE_HOST(host_flash_attention2_forward)<128>(const float*, const float*, const float*, float*, float*, int,
                                                       int, int, TimerManager*);
 #else
 // CuPy face (same symbol as kernel_fa2_optimized_f16.cu:432-448).  The reference

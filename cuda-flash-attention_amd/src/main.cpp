@@ -1,7 +1,7 @@
 // main.cpp -- the FlashAttention CLI: file in, file out.
 //
 // Contract of detker/CUDA-Flash-Attention src/main.cpp:14-135:
-//   FlashAttention <naive|fa1|fa2> <forward|backward|forward_backward> <fp16|fp32> <dir/B{b}_H{h}_S{s}_D{d}>
+//   FlashAttention <naive|fa1|fa2> <forward|backward|forward_backward> <fp16|fp32|bf16> <dir/B{b}_H{h}_S{s}_D{d}>
 // reads Q.bin K.bin V.bin (+ O.bin logsumexp.bin in backward mode; dO.bin if
 // present, else dO = 1), writes O.bin logsumexp.bin and/or dQ.bin dK.bin dV.bin
 // into the same directory, and prints the kernel-only time (TimerManager).

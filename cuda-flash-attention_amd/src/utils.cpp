@@ -2,7 +2,7 @@
 // Behaviour of detker/CUDA-Flash-Attention src/utils.cpp:5-100: raw little-endian
 // fp32 files with no header, a short read/write or missing file exits through ERR,
 // the shape comes from the directory basename "B%d_H%d_S%d_D%d" (trailing '/'
-// ignored), argv is <naive|fa1|fa2> <forward|backward|forward_backward> <fp16|fp32> <dir>.
+// ignored), argv is <naive|fa1|fa2> <forward|backward|forward_backward> <fp16|fp32|bf16> <dir>.
 #include <sys/stat.h>
 
 #include <cstdio>
@@ -58,6 +58,7 @@ void parse_args(int argc, char** argv, ComputeDataType* precision, ComputeType* 
 
     if (!strcmp(argv[3], "fp16")) *precision = ComputeDataType::FP16;
     else if (!strcmp(argv[3], "fp32")) *precision = ComputeDataType::FP32;
+    else if (!strcmp(argv[3], "bf16")) *precision = ComputeDataType::BF16;
     else usage(argv[0]);
 
     *data_path = argv[4];

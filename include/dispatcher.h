@@ -44,6 +44,10 @@ struct FlashAttentionDispatcher {
         tm->AddMillis(ms);  // kernel time = max over devices
     }
 
+    static int c_precision(ComputeDataType prec) {
+        return prec == ComputeDataType::FP16 ? FA2_FP16 : prec == ComputeDataType::BF16 ? FA2_BF16 : FA2_FP32;
+    }
+
     static void dispatch_forward(const float* Q, const float* K, const float* V, float* O, float* lse, int B, int H,
                                  int S, ComputeDataType prec, ComputeType method, TimerManager* tm) {
         require_fa2(method);
@@ -51,13 +55,16 @@ struct FlashAttentionDispatcher {
         if (ndev > 1) {
             float ms = 0.f;
             const int rc = fa2_forward_host(Q, K, V, O, lse, B, H, S, HEAD_DIM,
-                                            prec == ComputeDataType::FP16 ? FA2_FP16 : FA2_FP32, ndev, &ms);
+                                            c_precision(prec), ndev, &ms);
             sharded(rc, ms, tm);
             return;
         }
         if (prec == ComputeDataType::FP16) {
             printf("Running Flash Attention 2 Forward (HEAD_DIM=%d) with FP16 tiles (MFMA)...\n", HEAD_DIM);
             host_flash_attention2_forward_fp16<HEAD_DIM>(Q, K, V, O, lse, B, S, H, tm);
+        } else if (prec == ComputeDataType::BF16) {
+            printf("Running Flash Attention 2 Forward (HEAD_DIM=%d) with BF16 tiles (MFMA)...\n", HEAD_DIM);
+            host_flash_attention2_forward_bf16<HEAD_DIM>(Q, K, V, O, lse, B, S, H, tm);
         } else {
             printf("Running Flash Attention 2 Forward (HEAD_DIM=%d)...\n", HEAD_DIM);
             host_flash_attention2_forward<HEAD_DIM>(Q, K, V, O, lse, B, S, H, tm);
@@ -72,13 +79,16 @@ struct FlashAttentionDispatcher {
         if (ndev > 1) {
             float ms = 0.f;
             const int rc = fa2_backward_host(Q, K, V, O, dO, lse, dQ, dK, dV, B, H, S, HEAD_DIM,
-                                             prec == ComputeDataType::FP16 ? FA2_FP16 : FA2_FP32, ndev, &ms);
+                                             c_precision(prec), ndev, &ms);
             sharded(rc, ms, tm);
             return;
         }
         if (prec == ComputeDataType::FP16) {
             printf("Running Flash Attention 2 Backward (HEAD_DIM=%d) with FP16 tiles (MFMA)...\n", HEAD_DIM);
             host_flash_attention2_backward_fp16<HEAD_DIM>(Q, K, V, O, dO, lse, dQ, dK, dV, B, S, H, tm);
+        } else if (prec == ComputeDataType::BF16) {
+            printf("Running Flash Attention 2 Backward (HEAD_DIM=%d) with BF16 tiles (MFMA)...\n", HEAD_DIM);
+            host_flash_attention2_backward_bf16<HEAD_DIM>(Q, K, V, O, dO, lse, dQ, dK, dV, B, S, H, tm);
         } else {
             printf("Running Flash Attention 2 Backward (HEAD_DIM=%d)...\n", HEAD_DIM);
             host_flash_attention2_backward<HEAD_DIM>(Q, K, V, O, dO, lse, dQ, dK, dV, B, S, H, tm);

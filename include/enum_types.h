@@ -16,5 +16,6 @@ enum class ModeType {
 // Precision of the on-chip (LDS/VGPR) tiles; HBM I/O is fp32 either way.
 enum class ComputeDataType {
     FP16,  // fp16 tiles, MFMA f16 -> fp32 accumulate
-    FP32   // fp32 tiles, exact-fp32 MFMA
+    FP32,  // fp32 tiles, exact-fp32 MFMA
+    BF16   // bf16 tiles, MFMA bf16 -> fp32 accumulate (extension: README.md:504-508)
 };

@@ -21,7 +21,7 @@
 inline void usage(char* name) {
     fprintf(stderr,
             "USAGE: %s <computation_method:naive|fa1|fa2> <mode:forward|backward|forward_backward> "
-            "<SHM_precision:fp16|fp32> <data_folder_path>\n",
+            "<SHM_precision:fp16|fp32|bf16> <data_folder_path>\n",
             name);
     exit(EXIT_FAILURE);
 }

@@ -14,7 +14,9 @@
  *
  * `precision` mirrors the reference's ComputeDataType (include/enum_types.h:15-18):
  *   FA2_FP32 -- fp32 tiles, exact-fp32 MFMA (the reference's default .cu files);
- *   FA2_FP16 -- fp16 tiles, MFMA f16 -> fp32 accumulate (the _f16.cu files).
+ *   FA2_FP16 -- fp16 tiles, MFMA f16 -> fp32 accumulate (the _f16.cu files);
+ *   FA2_BF16 -- bf16 tiles, MFMA bf16 -> fp32 accumulate (an extension: the
+ *               reference lists BF16 under "Possible Improvements", README.md:504-508).
  */
 #ifndef FA2_AMD_H
 #define FA2_AMD_H
@@ -23,7 +25,7 @@
 extern "C" {
 #endif
 
-enum { FA2_FP16 = 0, FA2_FP32 = 1 };
+enum { FA2_FP16 = 0, FA2_FP32 = 1, FA2_BF16 = 2 };
 
 enum {
     FA2_OK = 0,

@@ -80,7 +80,7 @@ def test_python_api_refuses_cpu_tensors():
     ([], "USAGE"),
     (["fa3", "forward", "fp32", "x/B1_H1_S8_D64"], "USAGE"),
     (["fa2", "both", "fp32", "x/B1_H1_S8_D64"], "USAGE"),
-    (["fa2", "forward", "bf16", "x/B1_H1_S8_D64"], "USAGE"),
+    (["fa2", "forward", "fp8", "x/B1_H1_S8_D64"], "USAGE"),
     (["fa2", "forward", "fp32", "x/not_a_shape"], "sscanf"),
 ])
 def test_cli_argv_contract(argv, needle):
@@ -102,6 +102,20 @@ def test_cupy_face_compiles_under_hiprtc(fname, symbols):
     exported = rawmodule.exported_kernels(co)
     for s in symbols:
         assert s in exported
+
+
+@pytest.mark.parametrize("fname,symbols", [
+    ("kernel_fa2_optimized_f16.cu", ["flash_attention2_forward_kernel_wrapper"]),
+    ("f-attn2-backward_f16.cu", ["D_computation_reduction_kernel_wrapper", "flash_attention2_backward_kernel_wrapper"]),
+])
+def test_cupy_face_bf16_compiles_under_hiprtc(fname, symbols):
+    """The _f16 files' text with -DFA2_TILE_BF16 added: the same symbols, bf16 MFMA."""
+    co = rawmodule.compile_source(rawmodule.load_kernel_source(fname),
+                                  tuple(rawmodule.HARNESS_OPTIONS) + ("-DFA2_TILE_BF16",))
+    exported = rawmodule.exported_kernels(co)
+    for s in symbols:
+        assert s in exported
+    assert co != rawmodule.compile_source(rawmodule.load_kernel_source(fname))  # a different tile type
 
 
 @pytest.mark.parametrize("suffix", ["", "_f16"])
