@@ -11,7 +11,9 @@
 #include <thread>
 #include <vector>
 
+#include "f-attn.cuh"
 #include "f-attn2.cuh"
+#include "vanilla-attn.cuh"
 
 namespace {
 
@@ -153,6 +155,22 @@ int fa2_backward_dq(const float* q, const float* k, const float* v, const float*
     return hip_status(
         fa2::launch_bwd_dq_f16(D, q, k, v, dout, lse, delta, dq, B * H, S, static_cast<hipStream_t>(stream)),
         "fa2_backward_dq launch");
+}
+
+int fa2_naive_forward(const float* q, const float* k, const float* v, float* o, float* lse, float* scores, int B,
+                      int H, int S, int D, void* stream) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_ptrs({q, k, v, o, scores}))) return rc;
+    return hip_status(fa2::launch_vanilla_forward(D, q, k, v, o, lse, scores, B * H, S, static_cast<hipStream_t>(stream)),
+                      "fa2_naive_forward launch");
+}
+
+int fa2_fa1_forward(const float* q, const float* k, const float* v, float* o, float* l, float* m, int B, int H, int S,
+                    int D, void* stream) {
+    int rc;
+    if ((rc = check_shape(B, H, S, D)) || (rc = check_ptrs({q, k, v, o, l, m}))) return rc;
+    return hip_status(fa2::launch_fa1_forward(D, q, k, v, o, l, m, B * H, S, static_cast<hipStream_t>(stream)),
+                      "fa2_fa1_forward launch");
 }
 
 int fa2_backward_dq_delta(const float* q, const float* k, const float* v, const float* o, const float* dout,

@@ -33,6 +33,7 @@ SUPPORTED_HEAD_DIMS = (32, 64, 128)
 # exported symbols of include/fa2_amd.h (checked by tests/test_capi_symbols.py)
 C_SYMBOLS = (
     "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv", "fa2_backward_dq", "fa2_backward_dq_delta",
+    "fa2_naive_forward", "fa2_fa1_forward",
     "fa2_forward_host", "fa2_backward_host", "fa2_shard_range", "fa2_last_error",
     "fa2_version", "fa2_device_count",
 )
@@ -87,6 +88,8 @@ def _load(path):
         "fa2_backward_dkdv": [P] * 8 + [I] * 4 + [V],
         "fa2_backward_dq": [P] * 7 + [I] * 4 + [V],
         "fa2_backward_dq_delta": [P] * 8 + [I] * 4 + [V],
+        "fa2_naive_forward": [P] * 6 + [I] * 4 + [V],
+        "fa2_fa1_forward": [P] * 6 + [I] * 4 + [V],
         "fa2_forward_host": [P] * 5 + [I] * 6 + [FP],
         "fa2_backward_host": [P] * 9 + [I] * 6 + [FP],
         "fa2_shard_range": [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)],
@@ -210,6 +213,35 @@ def backward_dq_delta(q, k, v, o, dout, lse, delta_buf, dq, stream=None):
     ptrs = [_dev(t, n) for t, n in zip((q, k, v, o, dout, lse, delta_buf, dq),
                                        ("q", "k", "v", "o", "dout", "lse", "delta", "dq"))]
     _check(lib().fa2_backward_dq_delta(*ptrs, B, H, S, D, _stream(stream, q.device)))
+
+
+def naive_forward(q, k, v, out=None, lse=None, scores=None, stream=None):
+    """(O, LSE, P) of the naive baseline (the reference's vanilla attention, CLI
+    method ``naive``): the [B, H, S, S] score matrix is materialised (``scores``
+    ends holding P).  fp32 only, forward only, as in the reference."""
+    import torch
+
+    B, H, S, D = _shape(q)
+    out = torch.empty_like(q) if out is None else out
+    lse = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if lse is None else lse
+    scores = torch.empty((B, H, S, S), device=q.device, dtype=torch.float32) if scores is None else scores
+    ptrs = [_dev(t, n) for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out"), (lse, "lse"), (scores, "scores"))]
+    _check(lib().fa2_naive_forward(*ptrs, B, H, S, D, _stream(stream, q.device)))
+    return out, lse, scores
+
+
+def fa1_forward(q, k, v, out=None, l=None, m=None, stream=None):
+    """(O, l, m) of the FlashAttention-1 baseline (CLI method ``fa1``): l is the row
+    sum relative to m (the reference's ``logsumexp`` output), so LSE = m + ln l."""
+    import torch
+
+    B, H, S, D = _shape(q)
+    out = torch.empty_like(q) if out is None else out
+    l = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if l is None else l
+    m = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if m is None else m
+    ptrs = [_dev(t, n) for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out"), (l, "l"), (m, "m"))]
+    _check(lib().fa2_fa1_forward(*ptrs, B, H, S, D, _stream(stream, q.device)))
+    return out, l, m
 
 
 # ---------------------------------------------------------------------------

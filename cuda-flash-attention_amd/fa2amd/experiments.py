@@ -1,0 +1,260 @@
+"""Harness-compatible experiment runs and reporting.
+
+Mirrors the reporting side of test_flash_attention2.py (detker/CUDA-Flash-Attention):
+
+* the test configurations (``create_test_configs``, :1365-1405; the sequence-length
+  sweep B4_H8_D64, S = 128..4096, :1431-1460);
+* one row per (config, kernel) with the harness's metrics (:569-606) and pass rule
+  (max-abs < tolerance, no NaN/Inf, :1018-1020), PyTorch CPU / GPU reference rows
+  as there (:955-993);
+* ``experiment_results.csv`` with the harness's exact columns (:1108-1122) and the
+  kernel-comparison plots (:1126-1287; matplotlib only, the reference's seaborn
+  styling is not installed here).
+
+Kernels: ``fa2`` (the C ABI, precision fp32 / fp16 / bf16), ``fa1`` and
+``vanilla-attn`` (the comparison baselines, fp32 forward).  Expected values are the
+harness's own PyTorch-CPU reference computation (``compute_reference``, :197-208;
+backward by autograd with dO = ones, :220-232).
+
+    PYTHONPATH=cuda-flash-attention_amd python -m fa2amd.experiments --mode forward --experiment \
+        --save-results --output-dir out/
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import os
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+CSV_COLUMNS = ["Test", "Kernel", "Type", "Batch", "Heads", "SeqLen", "HeadDim", "Status", "MaxError", "MeanError",
+               "MSE", "MaxRelError", "KernelTime_ms", "TorchTime_ms", "Speedup", "TFLOPS", "Bandwidth_GBps",
+               "ErrorMessage"]
+
+# test_flash_attention2.py:1371-1399 (name, B, H, S, D)
+TEST_CONFIGS = [
+    ("Small-1", 1, 1, 128, 64), ("Small-2", 2, 4, 256, 64), ("Small-3", 2, 8, 256, 64),
+    ("Medium-1", 2, 8, 512, 64), ("Medium-2", 4, 8, 512, 64),
+    ("Large-1", 2, 8, 1024, 64), ("Large-2", 4, 12, 1024, 64),
+    ("Edge-NonPowerOf2", 8, 16, 100, 64), ("Edge-SmallSeq", 8, 16, 32, 64),
+    ("Stress-1", 8, 16, 2048, 64),
+]
+SEQLEN_SWEEP = (128, 256, 512, 1024, 2048, 4096)
+FORWARD_KERNELS = ("vanilla-attn", "fa1", "fa2")
+
+
+@dataclass
+class Row:
+    test: str
+    kernel: str
+    type: str
+    B: int
+    H: int
+    S: int
+    D: int
+    passed: bool = True
+    metrics: dict = field(default_factory=dict)
+    kernel_ms: float = 0.0
+    torch_ms: float = 0.0
+    error: str = ""
+
+    def as_csv(self):
+        m = self.metrics
+        return {"Test": self.test, "Kernel": self.kernel.upper(), "Type": self.type.upper()[:3], "Batch": self.B,
+                "Heads": self.H, "SeqLen": self.S, "HeadDim": self.D, "Status": "PASS" if self.passed else "FAIL",
+                "MaxError": m.get("max_abs_error", 0.0), "MeanError": m.get("mean_abs_error", 0.0),
+                "MSE": m.get("mse", 0.0), "MaxRelError": m.get("max_rel_error", 0.0), "KernelTime_ms": self.kernel_ms,
+                "TorchTime_ms": self.torch_ms, "Speedup": m.get("speedup", 0.0), "TFLOPS": m.get("tflops", 0.0),
+                "Bandwidth_GBps": m.get("bandwidth_gbps", 0.0), "ErrorMessage": self.error}
+
+
+def harness_inputs(B, H, S, D, seed=42):
+    """The harness's synthetic inputs (generate_test_data(None, cfg), :182-195)."""
+    import torch
+
+    g = torch.Generator().manual_seed(seed)
+    return tuple(torch.rand(B, H, S, D, generator=g) for _ in range(3))
+
+
+def torch_reference(q, k, v):
+    """compute_reference (:197-208): softmax(Q K^T / sqrt(D)) V on the CPU, and its time."""
+    import torch
+
+    t0 = time.perf_counter()
+    s = torch.matmul(q, k.transpose(-2, -1)) / (q.shape[-1] ** 0.5)
+    o = torch.matmul(torch.softmax(s, dim=-1), v)
+    return o, (time.perf_counter() - t0) * 1e3
+
+
+def torch_reference_backward(q, k, v):
+    """compute_reference_backward (:220-232): autograd of sum(O) (dO = ones)."""
+    import torch
+
+    qq, kk, vv = (x.clone().requires_grad_() for x in (q, k, v))
+    t0 = time.perf_counter()
+    o = torch.matmul(torch.softmax(torch.matmul(qq, kk.transpose(-2, -1)) / (q.shape[-1] ** 0.5), dim=-1), vv)
+    o.backward(torch.ones_like(o))
+    ms = (time.perf_counter() - t0) * 1e3
+    return o.detach(), (qq.grad, kk.grad, vv.grad), ms
+
+
+def _gpu_time(fn, runs=10):
+    import torch
+
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(runs):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / runs
+
+
+def run_forward(name, B, H, S, D, kernels, precision="fp32", tolerance=1e-3):
+    import torch
+
+    import fa2amd
+    from . import harness
+
+    q, k, v = harness_inputs(B, H, S, D)
+    exp, torch_ms = torch_reference(q, k, v)
+    exp = exp.numpy()
+    rows = [Row(name, "pytorch cpu", "forward", B, H, S, D, True,
+                {**harness.compute_metrics(exp, exp, torch_ms, torch_ms, B, H, S, D), "speedup": 1.0},
+                torch_ms, torch_ms)]
+    tq, tk, tv = (x.cuda() for x in (q, k, v))
+    gpu_ms = _gpu_time(lambda: torch.nn.functional.scaled_dot_product_attention(tq, tk, tv))
+    og = torch.nn.functional.scaled_dot_product_attention(tq, tk, tv).cpu().numpy()
+    rows.append(Row(name, "pytorch gpu", "forward", B, H, S, D, True,
+                    harness.compute_metrics(og, exp, gpu_ms, torch_ms, B, H, S, D), gpu_ms, torch_ms))
+    for kern in kernels:
+        try:
+            if kern == "fa2":
+                o = torch.empty_like(tq)
+                lse = torch.empty((B, H, S), device=tq.device)
+                ms = _gpu_time(lambda: fa2amd.forward(tq, tk, tv, precision, out=o, lse=lse))
+            elif kern == "fa1":
+                o, l, m = fa2amd.fa1_forward(tq, tk, tv)
+                ms = _gpu_time(lambda: fa2amd.fa1_forward(tq, tk, tv, out=o, l=l, m=m))
+            elif kern == "vanilla-attn":
+                o, lse, p = fa2amd.naive_forward(tq, tk, tv)
+                ms = _gpu_time(lambda: fa2amd.naive_forward(tq, tk, tv, out=o, lse=lse, scores=p))
+            else:
+                raise ValueError(f"unknown kernel {kern}")
+            got = o.cpu().numpy()
+            met = harness.compute_metrics(got, exp, ms, torch_ms, B, H, S, D)
+            label = kern if (kern != "fa2" or precision == "fp32") else f"fa2-{precision}"
+            rows.append(Row(name, label, "forward", B, H, S, D, harness.passed(met, got, tolerance), met, ms,
+                            torch_ms))
+        except Exception as e:  # recorded as a FAIL row, as the harness does (:1030-1046)
+            rows.append(Row(name, kern, "forward", B, H, S, D, False, {}, 0.0, torch_ms, str(e)))
+    return rows
+
+
+def run_backward(name, B, H, S, D, precision="fp32", tolerance=1e-3):
+    import fa2amd
+    from . import harness
+
+    q, k, v = harness_inputs(B, H, S, D)
+    o_ref, grads_ref, torch_ms = torch_reference_backward(q, k, v)
+    exp = np.concatenate([g.numpy().ravel() for g in grads_ref])
+    r = harness.FA2Runner(precision)
+    out, lse, _ = r.run_fa2_forward_kernel(q, k, v)
+    grads, ms = r.run_cuda_fa2_backward_kernel(q, k, v, out, np.ones_like(out), lse)
+    got = np.concatenate([grads[n].ravel() for n in ("dQ", "dK", "dV")])
+    met = harness.compute_metrics(got, exp, ms, torch_ms, B, H, S, D)
+    flops = 2.5 * 4 * B * H * S * S * D  # the harness's backward accounting (:634)
+    met["tflops"] = flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    label = "fa2" if precision == "fp32" else f"fa2-{precision}"
+    return [Row(name, label, "backward", B, H, S, D, harness.passed(met, got, tolerance), met, ms, torch_ms)]
+
+
+def write_csv(rows, path):
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=CSV_COLUMNS)
+        w.writeheader()
+        for r in rows:
+            w.writerow(r.as_csv())
+
+
+def plot(rows, out_dir):
+    """kernel_comparison.png: time and TFLOPS per test and kernel (the harness's
+    _generate_plots panels, :1126-1200).  Skipped if matplotlib is unavailable."""
+    try:
+        import matplotlib
+
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+    except ImportError:
+        return None
+    ok = [r for r in rows if r.passed and r.kernel_ms > 0]
+    tests = list(dict.fromkeys(r.test for r in ok))
+    kernels = list(dict.fromkeys(r.kernel for r in ok))
+    fig, axes = plt.subplots(1, 2, figsize=(14, 5))
+    for kern in kernels:
+        xs = [tests.index(r.test) for r in ok if r.kernel == kern]
+        axes[0].plot(xs, [r.kernel_ms for r in ok if r.kernel == kern], marker="o", label=kern.upper())
+        axes[1].plot(xs, [r.metrics.get("tflops", 0) for r in ok if r.kernel == kern], marker="o",
+                     label=kern.upper())
+    for ax, title in zip(axes, ("Kernel time (ms)", "TFLOPS")):
+        ax.set_xticks(range(len(tests)))
+        ax.set_xticklabels(tests, rotation=45, ha="right")
+        ax.set_title(title)
+        ax.grid(True, alpha=0.3)
+        ax.legend()
+    axes[0].set_yscale("log")
+    fig.tight_layout()
+    path = os.path.join(out_dir, "kernel_comparison.png")
+    fig.savefig(path, dpi=120)
+    plt.close(fig)
+    return path
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--mode", choices=["forward", "backward"], default="forward")
+    ap.add_argument("--kernel", choices=["fa2", "fa1", "vanilla-attn"], default="fa2")
+    ap.add_argument("--precision", choices=["fp32", "fp16", "bf16"], default="fp32")
+    ap.add_argument("--experiment", action="store_true", help="every kernel on every test config")
+    ap.add_argument("--seqlen-experiment", action="store_true", help="B4_H8_D64, S = 128..4096")
+    ap.add_argument("--tolerance", type=float, default=1e-3)
+    ap.add_argument("--configs", default="", help="comma-separated subset of config names")
+    ap.add_argument("--save-results", action="store_true")
+    ap.add_argument("--output-dir", default="./experiment_results")
+    args = ap.parse_args(argv)
+
+    if args.seqlen_experiment:
+        configs = [(f"SeqLen-S{s}", 4, 8, s, 64) for s in SEQLEN_SWEEP]
+    else:
+        configs = TEST_CONFIGS
+    if args.configs:
+        keep = set(args.configs.split(","))
+        configs = [c for c in configs if c[0] in keep]
+    kernels = FORWARD_KERNELS if (args.experiment or args.seqlen_experiment) else (args.kernel,)
+    if args.mode == "backward" and kernels != ("fa2",) and not args.experiment:
+        ap.error(f"Only 'fa2' kernel supports backward pass. Got --kernel={args.kernel}")  # :1494-1495
+
+    rows = []
+    for name, B, H, S, D in configs:
+        if args.mode == "forward":
+            rows += run_forward(name, B, H, S, D, kernels, args.precision, args.tolerance)
+        else:
+            rows += run_backward(name, B, H, S, D, args.precision, args.tolerance)
+        for r in rows[-(len(kernels) + 2 if args.mode == "forward" else 1):]:
+            print(f"{r.test:18s} {r.kernel.upper():14s} {r.type[:3].upper()} {'PASS' if r.passed else 'FAIL'} "
+                  f"max_err {r.metrics.get('max_abs_error', float('nan')):.3e} {r.kernel_ms:9.4f} ms "
+                  f"{r.metrics.get('tflops', 0.0):8.3f} TFLOPS {r.error}", flush=True)
+    if args.save_results:
+        os.makedirs(args.output_dir, exist_ok=True)
+        name = "experiment_results.csv" if args.mode == "forward" else "backward_experiment_results.csv"
+        write_csv(rows, os.path.join(args.output_dir, name))
+        plot(rows, args.output_dir)
+    return 0 if all(r.passed for r in rows) else 1
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

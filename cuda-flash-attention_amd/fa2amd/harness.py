@@ -15,6 +15,10 @@ Two back ends:
 * ``FA2Runner``     -- the C ABI (libfa2amd.so), precision "fp32" or "fp16";
 * ``RawModuleRunner`` -- the reference-named kernel files compiled from source
   text with hiprtc and launched with the harness's exact geometry (CuPy face).
+
+and, for the harness's comparison kernels (``--kernel fa1|vanilla-attn``),
+``BaselineRawRunner.run_cuda_fa1_kernel`` / ``run_cuda_naive_kernel`` (:315-372,
+:428-474) over kernels/f-attn.cu and kernels/vanilla-attn.cu.
 """
 from __future__ import annotations
 
@@ -137,6 +141,66 @@ class RawModuleRunner:
         end.synchronize()
         grads = {"dQ": dq.cpu().numpy(), "dK": dk.cpu().numpy(), "dV": dv.cpu().numpy()}
         return grads, start.elapsed_time(end) / NUM_RUNS
+
+
+class BaselineRawRunner:
+    """The harness's FA1 and naive-attention runs (test_flash_attention2.py:315-372,
+    :428-474): kernels/f-attn.cu and kernels/vanilla-attn.cu compiled from text,
+    grid B*H, 256 / 128 threads, zero-filled outputs, head_dim 64 (the wrappers'
+    fixed D, as in the reference).  Each returns ``(output_np, elapsed_ms)``."""
+
+    def __init__(self):
+        from .rawmodule import RawModule, load_kernel_source
+
+        self.fa1_mod = RawModule(load_kernel_source("f-attn.cu"),
+                                 name_expressions=("flash_attention_forward_kernel_wrapper",))
+        self.naive_mod = RawModule(load_kernel_source("vanilla-attn.cu"),
+                                   name_expressions=("vanilla_attention_kernel_wrapper",))
+        self.fa1_kernel = self.fa1_mod.get_function("flash_attention_forward_kernel_wrapper")
+        self.naive_kernel = self.naive_mod.get_function("vanilla_attention_kernel_wrapper")
+
+    @staticmethod
+    def _timed(fn):
+        import torch
+
+        fn()
+        torch.cuda.synchronize()
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record()
+        for _ in range(NUM_RUNS):
+            fn()
+        end.record()
+        end.synchronize()
+        return start.elapsed_time(end) / NUM_RUNS
+
+    def run_cuda_fa1_kernel(self, Q, K, V):
+        import torch
+
+        B, H, S, D = Q.shape
+        if D != 64:
+            raise ValueError("the FA1 wrapper is instantiated for head_dim 64 (f-attn.cu:295 in the reference)")
+        q, k, v = _to_dev(Q), _to_dev(K), _to_dev(V)
+        o = torch.zeros_like(q)
+        lse = torch.zeros((B, H, S), device=q.device, dtype=torch.float32)
+        maxes = torch.zeros((B, H, S), device=q.device, dtype=torch.float32)
+        shared_mem = (32 * D * 2 + 32 * D * 2 + 32 * 32 + 32 * 2) * 4  # :338-341
+        ms = self._timed(lambda: self.fa1_kernel((B * H,), (256,), (q, k, v, o, lse, maxes, B, H, S),
+                                                 shared_mem=shared_mem))
+        self.last_l, self.last_m = lse.cpu().numpy(), maxes.cpu().numpy()
+        return o.cpu().numpy(), ms
+
+    def run_cuda_naive_kernel(self, Q, K, V):
+        import torch
+
+        B, H, S, D = Q.shape
+        if D != 64:
+            raise ValueError("the naive wrapper is instantiated for head_dim 64 (vanilla-attn.cu:156 in the reference)")
+        q, k, v = _to_dev(Q), _to_dev(K), _to_dev(V)
+        attn = torch.zeros((B, H, S, S), device=q.device, dtype=torch.float32)
+        o = torch.zeros_like(q)
+        ms = self._timed(lambda: self.naive_kernel((B * H,), (128,), (q, k, v, o, attn, B, H, S)))
+        self.last_p = attn.cpu().numpy()
+        return o.cpu().numpy(), ms
 
 
 def compute_metrics(actual, expected, kernel_time_ms, torch_time_ms, B, H, S, D):

@@ -24,6 +24,7 @@ int main(int argc, char** argv) {
 
     int B, H, S, D;
     parse_config_string(data_path, &B, &H, &S, &D);
+    check_method_support(method, mode, precision);
 
     // (argv is validated before the device timer is created, so a bad command
     // line fails the same way on a host without a GPU)

@@ -5,9 +5,10 @@
 // FlashAttentionDispatcher (:11-104) and RuntimeDimDispatcher (:107-141):
 // head_dim is matched by doubling from 32 (here up to 128); forward_backward runs
 // the forward then the backward, O and LSE passing through host memory exactly
-// as there (:91-104).  Only FlashAttention2 is built (SURVEY §2 marks the naive /
-// FA1 baselines out of scope); asking for them exits(1) with a message, as the
-// reference does for its own unsupported combinations (:30-47, :74-83).
+// as there (:91-104).  Methods: fa2 (fp32 / fp16 / bf16 tiles, forward and
+// backward), fa1 and naive (the comparison baselines, kernels/f-attn.cu and
+// kernels/vanilla-attn.cu: fp32 forward only, with the reference's messages and
+// exit(1) for the other combinations, :30-47, :74-83).
 //
 // FA2_NUM_DEVICES=N (environment) shards the B*H heads over N GPUs through the C
 // ABI's host API (fa2_amd.h), one host thread per device, no collective.
@@ -18,7 +19,9 @@
 #include <utility>
 
 #include "enum_types.h"
+#include "f-attn.cuh"
 #include "f-attn2.cuh"
+#include "vanilla-attn.cuh"
 #include "fa2_amd.h"
 #include "timer.h"
 
@@ -28,11 +31,56 @@ inline int fa2_env_devices() {
     return n < 1 ? 1 : n;
 }
 
+// The baselines' unsupported combinations, with the reference's messages
+// (dispatcher.h:31-50, 74-83 there).  The dispatcher reaches the same exits; the
+// CLI calls this right after argv parsing, before any device work.
+inline void check_method_support(ComputeType method, ModeType mode, ComputeDataType prec) {
+    if (method == ComputeType::FlashAttention2) return;
+    const bool fa1 = method == ComputeType::FlashAttention1;
+    if (mode != ModeType::Backward && prec != ComputeDataType::FP32) {
+        fprintf(stderr, fa1 ? "Error: Flash Attention 1 FP16 support not implemented\n"
+                            : "Error: Vanilla Attention FP16 support not implemented\n");
+        exit(EXIT_FAILURE);
+    }
+    if (mode != ModeType::Forward) {
+        fprintf(stderr, fa1 ? "Error: Flash Attention 1 backward pass not implemented\n"
+                            : "Error: Vanilla Attention backward pass not implemented\n");
+        exit(EXIT_FAILURE);
+    }
+}
+
 template <int HEAD_DIM>
 struct FlashAttentionDispatcher {
-    static void require_fa2(ComputeType m) {
-        if (m != ComputeType::FlashAttention2) {
-            fprintf(stderr, "Error: only the fa2 method is part of this build (naive/fa1 are reference baselines)\n");
+    // fa1 / naive forward (fp32 only, as the reference, dispatcher.h:31-50); true if handled
+    static bool baseline_forward(const float* Q, const float* K, const float* V, float* O, float* lse, int B, int H,
+                                 int S, ComputeDataType prec, ComputeType method, TimerManager* tm) {
+        if (method == ComputeType::FlashAttention1) {
+            if (prec != ComputeDataType::FP32) {
+                fprintf(stderr, "Error: Flash Attention 1 FP16 support not implemented\n");
+                exit(EXIT_FAILURE);
+            }
+            printf("Running Flash Attention 1 Forward (HEAD_DIM=%d)...\n", HEAD_DIM);
+            host_flash_attention_forward<HEAD_DIM>(Q, K, V, O, lse, B, S, H, tm);
+            return true;
+        }
+        if (method == ComputeType::Naive) {
+            if (prec != ComputeDataType::FP32) {
+                fprintf(stderr, "Error: Vanilla Attention FP16 support not implemented\n");
+                exit(EXIT_FAILURE);
+            }
+            printf("Running Vanilla Attention Forward (HEAD_DIM=%d)...\n", HEAD_DIM);
+            host_vanilla_attention_forward<HEAD_DIM>(Q, K, V, O, lse, B, S, H, tm);
+            return true;
+        }
+        return false;
+    }
+    static void require_fa2_backward(ComputeType m) {
+        if (m == ComputeType::FlashAttention1) {
+            fprintf(stderr, "Error: Flash Attention 1 backward pass not implemented\n");
+            exit(EXIT_FAILURE);
+        }
+        if (m == ComputeType::Naive) {
+            fprintf(stderr, "Error: Vanilla Attention backward pass not implemented\n");
             exit(EXIT_FAILURE);
         }
     }
@@ -50,7 +98,7 @@ struct FlashAttentionDispatcher {
 
     static void dispatch_forward(const float* Q, const float* K, const float* V, float* O, float* lse, int B, int H,
                                  int S, ComputeDataType prec, ComputeType method, TimerManager* tm) {
-        require_fa2(method);
+        if (baseline_forward(Q, K, V, O, lse, B, H, S, prec, method, tm)) return;
         const int ndev = fa2_env_devices();
         if (ndev > 1) {
             float ms = 0.f;
@@ -74,7 +122,7 @@ struct FlashAttentionDispatcher {
     static void dispatch_backward(const float* Q, const float* K, const float* V, const float* O, const float* dO,
                                   const float* lse, float* dQ, float* dK, float* dV, int B, int H, int S,
                                   ComputeDataType prec, ComputeType method, TimerManager* tm) {
-        require_fa2(method);
+        require_fa2_backward(method);
         const int ndev = fa2_env_devices();
         if (ndev > 1) {
             float ms = 0.f;

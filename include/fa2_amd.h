@@ -75,6 +75,18 @@ int fa2_backward_dq_delta(const float* q, const float* k, const float* v, const 
                           const float* lse, float* delta, float* dq, int batch, int heads, int seq, int head_dim,
                           void* stream);
 
+/* Comparison baselines, exact fp32, forward only, one workgroup per
+ * (b, h) as in the reference.
+ *   fa2_naive_forward: the reference's vanilla attention (kernels/vanilla-attn.cu:7-70,
+ *     CLI method `naive`): scores [B,H,S,S] materialised in `scores` (left holding P),
+ *     O, and LSE (may be NULL; the reference writes none).
+ *   fa2_fa1_forward: FlashAttention-1 (kernels/f-attn.cu:18-207, CLI method `fa1`):
+ *     O, l (row sum relative to m, the reference's `logsumexp` output) and m. */
+int fa2_naive_forward(const float* q, const float* k, const float* v, float* o, float* lse, float* scores, int batch,
+                      int heads, int seq, int head_dim, void* stream);
+int fa2_fa1_forward(const float* q, const float* k, const float* v, float* o, float* l, float* m, int batch,
+                    int heads, int seq, int head_dim, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Host-pointer API: the reference host functions' semantics
  * (kernel_fa2_optimized.cu:350-423, f-attn2-backward.cu:384-485): host buffers

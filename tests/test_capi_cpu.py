@@ -105,6 +105,37 @@ def test_cupy_face_compiles_under_hiprtc(fname, symbols):
 
 
 @pytest.mark.parametrize("fname,symbols", [
+    ("f-attn.cu", ["flash_attention_forward_kernel_wrapper"]),
+    ("vanilla-attn.cu", ["vanilla_attention_kernel_wrapper"]),
+])
+def test_baseline_cupy_face_compiles_under_hiprtc(fname, symbols):
+    """The harness's comparison kernels (test_flash_attention2.py:77-78, 147-170)."""
+    co = rawmodule.compile_source(rawmodule.load_kernel_source(fname))
+    exported = rawmodule.exported_kernels(co)
+    for s in symbols:
+        assert s in exported
+
+
+@pytest.mark.parametrize("argv,needle", [
+    (["fa1", "backward", "fp32", "x/B1_H1_S8_D64"], "Flash Attention 1 backward pass not implemented"),
+    (["naive", "forward_backward", "fp32", "x/B1_H1_S8_D64"], "Vanilla Attention backward pass not implemented"),
+    (["fa1", "forward", "fp16", "x/B1_H1_S8_D64"], "Flash Attention 1 FP16 support not implemented"),
+    (["naive", "forward", "fp16", "x/B1_H1_S8_D64"], "Vanilla Attention FP16 support not implemented"),
+])
+def test_cli_baseline_contract(tmp_path, argv, needle):
+    """The reference's messages for the baselines' unsupported combinations
+    (include/dispatcher.h:31-50, 74-83), reached before any GPU work (inputs exist)."""
+    d = tmp_path / "B1_H1_S8_D64"
+    d.mkdir()
+    for n in ("Q", "K", "V", "O", "logsumexp"):
+        np.zeros(8 * 64 if n != "logsumexp" else 8, np.float32).tofile(d / f"{n}.bin")
+    argv = argv[:3] + [str(d)]
+    r = subprocess.run([fa2amd.CLI_PATH] + argv, capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert needle in r.stderr
+
+
+@pytest.mark.parametrize("fname,symbols", [
     ("kernel_fa2_optimized_f16.cu", ["flash_attention2_forward_kernel_wrapper"]),
     ("f-attn2-backward_f16.cu", ["D_computation_reduction_kernel_wrapper", "flash_attention2_backward_kernel_wrapper"]),
 ])
@@ -132,3 +163,22 @@ def test_cupy_face_lds_budget(D, suffix):
     assert fwd["flash_attention2_forward_kernel_wrapper"] + dyn_fwd <= rawmodule.MAX_LDS_BYTES
     assert bwd["flash_attention2_backward_kernel_wrapper"] + dyn_bwd <= rawmodule.MAX_LDS_BYTES
     assert bwd["D_computation_reduction_kernel_wrapper"] + 64 * 4 <= rawmodule.MAX_LDS_BYTES
+
+
+def test_experiment_csv_columns(tmp_path):
+    """experiment_results.csv carries the harness's exact columns (test_flash_attention2.py:1108-1122;
+    the header of the reference's plots/experiment_results.csv)."""
+    from fa2amd import experiments
+
+    assert experiments.CSV_COLUMNS == [
+        "Test", "Kernel", "Type", "Batch", "Heads", "SeqLen", "HeadDim", "Status", "MaxError", "MeanError", "MSE",
+        "MaxRelError", "KernelTime_ms", "TorchTime_ms", "Speedup", "TFLOPS", "Bandwidth_GBps", "ErrorMessage"]
+    rows = [experiments.Row("Small-1", "fa2", "forward", 1, 1, 128, 64, True,
+                            {"max_abs_error": 1e-7, "tflops": 0.5}, 0.01, 1.0),
+            experiments.Row("Small-1", "fa1", "forward", 1, 1, 128, 64, False, {}, 0.0, 1.0, "boom")]
+    p = tmp_path / "experiment_results.csv"
+    experiments.write_csv(rows, str(p))
+    lines = p.read_text().splitlines()
+    assert lines[0].split(",") == experiments.CSV_COLUMNS
+    assert lines[1].startswith("Small-1,FA2,FOR,1,1,128,64,PASS,")
+    assert lines[2].startswith("Small-1,FA1,FOR,1,1,128,64,FAIL,") and lines[2].endswith("boom")
