@@ -11,8 +11,9 @@ Mirrors the reporting side of test_flash_attention2.py (detker/CUDA-Flash-Attent
   kernel-comparison plots (:1126-1287; matplotlib only, the reference's seaborn
   styling is not installed here).
 
-Kernels: ``fa2`` (the C ABI, precision fp32 / fp16 / bf16), ``fa1`` and
-``vanilla-attn`` (the comparison baselines, fp32 forward).  Expected values are the
+Kernels: ``fa2`` (the C ABI, precision fp32 / fp16 / bf16), ``fa1``, ``vanilla-attn``
+(the comparison baselines, fp32 forward, C ABI) and ``fa2-naive`` (kernels/plain-attn.cu
+through its CuPy face, head_dim 64).  Expected values are the
 harness's own PyTorch-CPU reference computation (``compute_reference``, :197-208;
 backward by autograd with dO = ones, :220-232).
 
@@ -42,7 +43,7 @@ TEST_CONFIGS = [
     ("Stress-1", 8, 16, 2048, 64),
 ]
 SEQLEN_SWEEP = (128, 256, 512, 1024, 2048, 4096)
-FORWARD_KERNELS = ("vanilla-attn", "fa1", "fa2")
+FORWARD_KERNELS = ("fa2-naive", "vanilla-attn", "fa1", "fa2")  # the harness's experiment set + fa1
 
 
 @dataclass
@@ -114,6 +115,9 @@ def _gpu_time(fn, runs=10):
     return a.elapsed_time(b) / runs
 
 
+_BASELINE = None  # hiprtc-compiled baseline modules, built on first use
+
+
 def run_forward(name, B, H, S, D, kernels, precision="fp32", tolerance=1e-3):
     import torch
 
@@ -140,6 +144,14 @@ def run_forward(name, B, H, S, D, kernels, precision="fp32", tolerance=1e-3):
             elif kern == "fa1":
                 o, l, m = fa2amd.fa1_forward(tq, tk, tv)
                 ms = _gpu_time(lambda: fa2amd.fa1_forward(tq, tk, tv, out=o, l=l, m=m))
+            elif kern == "fa2-naive":
+                if D != 64:
+                    raise ValueError("fa2-naive is instantiated for head_dim 64 only")
+                global _BASELINE
+                if _BASELINE is None:
+                    _BASELINE = harness.BaselineRawRunner()
+                got, ms = _BASELINE.run_naive_fa2_kernel(q, k, v)
+                o = torch.from_numpy(got)
             elif kern == "vanilla-attn":
                 o, lse, p = fa2amd.naive_forward(tq, tk, tv)
                 ms = _gpu_time(lambda: fa2amd.naive_forward(tq, tk, tv, out=o, lse=lse, scores=p))
@@ -217,7 +229,7 @@ def plot(rows, out_dir):
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--mode", choices=["forward", "backward"], default="forward")
-    ap.add_argument("--kernel", choices=["fa2", "fa1", "vanilla-attn"], default="fa2")
+    ap.add_argument("--kernel", choices=["fa2", "fa1", "vanilla-attn", "fa2-naive"], default="fa2")
     ap.add_argument("--precision", choices=["fp32", "fp16", "bf16"], default="fp32")
     ap.add_argument("--experiment", action="store_true", help="every kernel on every test config")
     ap.add_argument("--seqlen-experiment", action="store_true", help="B4_H8_D64, S = 128..4096")

@@ -17,8 +17,9 @@ Two back ends:
   text with hiprtc and launched with the harness's exact geometry (CuPy face).
 
 and, for the harness's comparison kernels (``--kernel fa1|vanilla-attn``),
-``BaselineRawRunner.run_cuda_fa1_kernel`` / ``run_cuda_naive_kernel`` (:315-372,
-:428-474) over kernels/f-attn.cu and kernels/vanilla-attn.cu.
+``BaselineRawRunner.run_cuda_fa1_kernel`` / ``run_naive_fa2_kernel`` /
+``run_cuda_naive_kernel`` (:315-372, :374-426, :428-474) over kernels/f-attn.cu,
+kernels/plain-attn.cu and kernels/vanilla-attn.cu.
 """
 from __future__ import annotations
 
@@ -156,8 +157,11 @@ class BaselineRawRunner:
                                  name_expressions=("flash_attention_forward_kernel_wrapper",))
         self.naive_mod = RawModule(load_kernel_source("vanilla-attn.cu"),
                                    name_expressions=("vanilla_attention_kernel_wrapper",))
+        self.plain_mod = RawModule(load_kernel_source("plain-attn.cu"),
+                                   name_expressions=("flash_attention2_forward_kernel_wrapper",))
         self.fa1_kernel = self.fa1_mod.get_function("flash_attention_forward_kernel_wrapper")
         self.naive_kernel = self.naive_mod.get_function("vanilla_attention_kernel_wrapper")
+        self.forward_fa_naive = self.plain_mod.get_function("flash_attention2_forward_kernel_wrapper")
 
     @staticmethod
     def _timed(fn):
@@ -187,6 +191,24 @@ class BaselineRawRunner:
         ms = self._timed(lambda: self.fa1_kernel((B * H,), (256,), (q, k, v, o, lse, maxes, B, H, S),
                                                  shared_mem=shared_mem))
         self.last_l, self.last_m = lse.cpu().numpy(), maxes.cpu().numpy()
+        return o.cpu().numpy(), ms
+
+    def run_naive_fa2_kernel(self, Q, K, V):
+        """The harness's "fa2-naive" run (:374-426): kernels/plain-attn.cu, grid
+        B*H*ceil(S/32), 256 threads, VALU-only FA2."""
+        import torch
+
+        B, H, S, D = Q.shape
+        if D != 64:
+            raise ValueError("the plain FA2 wrapper is instantiated for head_dim 64 (plain-attn.cu:286)")
+        q, k, v = _to_dev(Q), _to_dev(K), _to_dev(V)
+        o = torch.zeros_like(q)
+        lse = torch.zeros((B, H, S), device=q.device, dtype=torch.float32)
+        shared_mem = (32 * D * 2 + 32 * D * 2 + 32 * 32 + 32 * 3) * 4  # :393-396
+        T_r = (S + 31) // 32
+        ms = self._timed(lambda: self.forward_fa_naive((B * H * T_r,), (256,), (q, k, v, o, lse, B, H, S),
+                                                       shared_mem=shared_mem))
+        self.last_lse = lse.cpu().numpy()
         return o.cpu().numpy(), ms
 
     def run_cuda_naive_kernel(self, Q, K, V):

@@ -107,6 +107,7 @@ def test_cupy_face_compiles_under_hiprtc(fname, symbols):
 @pytest.mark.parametrize("fname,symbols", [
     ("f-attn.cu", ["flash_attention_forward_kernel_wrapper"]),
     ("vanilla-attn.cu", ["vanilla_attention_kernel_wrapper"]),
+    ("plain-attn.cu", ["flash_attention2_forward_kernel_wrapper"]),
 ])
 def test_baseline_cupy_face_compiles_under_hiprtc(fname, symbols):
     """The harness's comparison kernels (test_flash_attention2.py:77-78, 147-170)."""

@@ -97,6 +97,9 @@ def test_cupy_face_fa1_and_naive(baseline_runner, shape):
     assert maxerr(out, eo) < TIGHT
     lse = baseline_runner.last_m.astype(np.float64) + np.log(baseline_runner.last_l.astype(np.float64))
     assert maxerr(lse, el) < TIGHT * 10
+    out, ms = baseline_runner.run_naive_fa2_kernel(Q, K, V)
+    assert ms > 0 and harness.passed(harness.compute_metrics(out, eo, ms, 1.0, B, H, S, D), out, 1e-3)
+    assert maxerr(out, eo) < 1e-5 and maxerr(baseline_runner.last_lse, el) < 1e-4
     out, ms = baseline_runner.run_cuda_naive_kernel(Q, K, V)
     assert ms > 0 and harness.passed(harness.compute_metrics(out, eo, ms, 1.0, B, H, S, D), out, 1e-3)
     assert maxerr(out, eo) < TIGHT
@@ -135,7 +138,7 @@ def test_experiment_run_writes_harness_csv(tmp_path):
     text = (tmp_path / "experiment_results.csv").read_text().splitlines()
     assert text[0].split(",") == experiments.CSV_COLUMNS
     kernels = {line.split(",")[1] for line in text[1:]}
-    assert {"FA2", "FA1", "VANILLA-ATTN", "PYTORCH CPU", "PYTORCH GPU"} <= kernels
+    assert {"FA2", "FA1", "VANILLA-ATTN", "FA2-NAIVE", "PYTORCH CPU", "PYTORCH GPU"} <= kernels
     assert all(",PASS," in line for line in text[1:])
     rc = experiments.main(["--mode", "backward", "--configs", "Small-2", "--precision", "fp16", "--tolerance", "1e-2",
                            "--save-results", "--output-dir", str(tmp_path)])
