@@ -37,7 +37,26 @@ def main():
     dl = fa2amd.delta(do, o)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
     flops = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "dqd": 2.0, "delta": 0.0, "bwd": 10.0, "step": 14.0,
-             "step3": 14.0}
+             "step3": 14.0, "step2s": 14.0, "step2r": 14.0}
+    s2 = torch.cuda.Stream(device=dev)
+
+    def two_stream_step(dkdv_first):
+        """fwd, delta, then dK/dV and dQ concurrently on two streams (joined)."""
+        cur = torch.cuda.current_stream(dev)
+        fa2amd.forward(q, k, v, "fp16", out=o, lse=lse, stream=cur)
+        fa2amd.delta(do, o, out=dl, stream=cur)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        s2.wait_event(ev)
+        if dkdv_first:
+            fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv, stream=s2)
+            fa2amd.backward_dq(q, k, v, do, lse, dl, dq, stream=cur)
+        else:
+            fa2amd.backward_dq(q, k, v, do, lse, dl, dq, stream=s2)
+            fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv, stream=cur)
+        ev2 = torch.cuda.Event()
+        ev2.record(s2)
+        cur.wait_event(ev2)
     calls = {
         "fwd": lambda: fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
         "dkdv": lambda: fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv),
@@ -49,11 +68,28 @@ def main():
                          fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
                          fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv)),
         "dqd": lambda: fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
+        # dK/dV and dQ on two streams after a separate delta kernel
+        "step2s": lambda: two_stream_step(True),
+        "step2r": lambda: two_stream_step(False),
         # the pre-fusion order: separate delta kernel, dK/dV, dQ
         "step3": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse), fa2amd.delta(do, o, out=dl),
                           fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv),
                           fa2amd.backward_dq(q, k, v, do, lse, dl, dq)),
     }
+    # the bench step captured once into a HIP graph and replayed
+    graph = None
+    if "stepg" in (args.kernel or []):
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            calls["step"]()  # warm (lazy init outside the capture)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=side):
+                calls["step"]()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        calls["stepg"] = graph.replay
+        flops["stepg"] = 14.0
     kernels = args.kernel or ["fwd", "dkdv", "dq"]
     variants = args.variant or [""]
     libs = args.lib or [None]
