@@ -63,10 +63,17 @@ __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
 }
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
 #else
 __device__ __forceinline__ _Float16 to_tile(float x) { return (_Float16)x; }
 __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 #endif
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -398,9 +405,142 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
 #define FA2_STAMP_ARG
 #endif
 
+// ---- dK, dV on v_mfma_f32_16x16x32 (FA2_TUNE_DKDV_MF=16) ------------------------
+// Same algorithm and data flow as dkdv_step; the wave's 32 keys are two 16-key
+// blocks nb.  Measured at the power cap on random data (tools/microbench/mfma_lds.hip):
+// 16x16x32 delivers 16 % more FLOPs per joule than 32x32x16 (it reads and writes a
+// quarter of the accumulator per instruction for half the FLOPs), +9 % with a
+// dK/dV-like exp/VALU mix beside it.
+// Operand maps (lane l, g = l >> 4): A[m = l & 15][k = 8g + j], B[k = 8g + j][n = l & 15],
+// C[m = 4g + i][n = l & 15].
+//   S / dP (m = query, n = key, k = d): A = Q / dO rows (row reads), B = K / V
+//     fragments in VGPRs; accumulators start at -lse2 / -delta of rows 4g + i.
+//   dV^T / dK^T (m = d, n = key, k = query): B = P / dS packed from the two query
+//     blocks mb: k-slot 8g + j <-> query 16 (j >> 2) + 4g + (j & 3); A = dO^T / Q^T
+//     by two 4-row transposed reads (rows 4g.. and 16 + 4g.., columns 16 md..).
+template <int D>
+struct DkdvState16 {
+    f16x8 kf[2][D / 32], vf[2][D / 32];  // [nb][ks]: K / V[key 16 nb + (l&15)][d 32 ks + 8g ..]
+    f32x4 dka[D / 16][2], dva[D / 16][2];  // [md][nb]: C[d 16 md + 4g + i][key 16 nb + (l&15)]
+};
+
+template <int D>
+struct FragOffsets16 {
+    int row[D / 32];   // row read: row (l & 15), columns 32 ks + 8g .. +7
+    int tr[D / 16][2];  // transposed read of block md: rows 4g + q / 16 + 4g + q, columns 16 md + 4p
+    __device__ __forceinline__ void init(int lane) {
+        const int i = lane & 15, g = lane >> 4, q = i >> 2, p4 = i & 3;
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) row[ks] = tile_off<D>(i, 32 * ks + 8 * g);
+#pragma unroll
+        for (int md = 0; md < D / 16; ++md) {
+            tr[md][0] = tile_off<D>(4 * g + q, 16 * md + 4 * p4);
+            tr[md][1] = tile_off<D>(16 + 4 * g + q, 16 * md + 4 * p4);
+        }
+    }
+    // A operand: rows r0 + (l & 15), k-step ks over columns
+    __device__ __forceinline__ f16x8 rowop(const _Float16* tile, int r0, int ks) const {
+        return lds_row8(tile + row[ks] + r0 * D);
+    }
+    // A operand (transposed): columns 16 md .. +15 on m, the 32 rows r0 .. r0+31 on k
+    // in the packed order 16 (j >> 2) + 4g + (j & 3)
+    __device__ __forceinline__ f16x8 trop(const _Float16* tile, int r0, int md) const {
+        return cat4(lds_tr4(tile + tr[md][0] + r0 * D), lds_tr4(tile + tr[md][1] + r0 * D));
+    }
+};
+
+template <int D, int ABL = 0, typename Mid>
+__device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
+                                            const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
+                                            int g, Mid&& mid) {
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+        if (qb == 1) mid();
+        f32x4 sa[2][2], da[2][2];  // [mb][nb]
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const f32x4 lv = *reinterpret_cast<const f32x4*>(nlse2 + qb * 32 + 16 * mb + 4 * g);
+            const f32x4 dv = *reinterpret_cast<const f32x4*>(ndel + qb * 32 + 16 * mb + 4 * g);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                sa[mb][nb] = lv;
+                da[mb][nb] = dv;
+            }
+        }
+        if (!(ABL & 16)) {
+#pragma unroll
+            for (int ks = 0; ks < D / 32; ++ks)
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb) {
+                    const f16x8 qa = fo.rowop(Qs, qb * 32 + 16 * mb, ks), doa = fo.rowop(dOs, qb * 32 + 16 * mb, ks);
+#pragma unroll
+                    for (int nb = 0; nb < 2; ++nb) {
+                        sa[mb][nb] = mfma16(qa, st.kf[nb][ks], sa[mb][nb]);
+                        da[mb][nb] = mfma16(doa, st.vf[nb][ks], da[mb][nb]);
+                    }
+                }
+        }
+        f16x8 pf[2], dsf[2];  // [nb], k-slot j <-> query 16 (j >> 2) + 4g + (j & 3)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float sv = sa[j >> 2][nb][j & 3], dvv = da[j >> 2][nb][j & 3];
+                if (ABL & 2) {
+                    pf[nb][j] = to_tile(sv);
+                    dsf[nb][j] = to_tile(dvv);
+                } else {
+                    const float pv = fast_exp2(sv);
+                    pf[nb][j] = to_tile(pv);
+                    dsf[nb][j] = to_tile(pv * dvv);
+                }
+            }
+        if (ABL & 8) {
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) asm volatile("" ::"v"(pf[nb]), "v"(dsf[nb]));
+            continue;
+        }
+#pragma unroll
+        for (int md = 0; md < D / 16; ++md) {
+            const f16x8 a_do = fo.trop(dOs, qb * 32, md), a_q = fo.trop(Qs, qb * 32, md);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                st.dva[md][nb] = mfma16(a_do, pf[nb], st.dva[md][nb]);
+                st.dka[md][nb] = mfma16(a_q, dsf[nb], st.dka[md][nb]);
+            }
+        }
+    }
+}
+
+// a wave's 32 keys x D results (16x16 accumulator layout) through its LDS stage,
+// stored as whole 128-B row segments
+template <int D>
+__device__ __forceinline__ void store_block_rows16(float (*os)[36], const f32x4 (&acc)[D / 16][2], float scale,
+                                                   float* __restrict__ dst, int rows_valid, int lane) {
+    const int i16 = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b) {
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                const f32x4 v = acc[2 * b + mh][nb] * scale;
+                *reinterpret_cast<f32x4*>(&os[16 * nb + i16][16 * mh + 4 * g]) = v;
+            }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const int row = 8 * s4 + (lane >> 3), c4 = (lane & 7) * 4;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(&os[row][c4]);
+            if (row < rows_valid) *reinterpret_cast<f32x4*>(dst + (long)row * D + 32 * b + c4) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // KB x 32 keys per wave, NW waves: grid BH * ceil(S / (32*KB*NW)), block 64*NW.
 // ABL: timing ablations (see dkdv_step; plus 1 = no staging in the loop, 4 = no barrier)
-template <int D, int NW, int KB = 1, int ABL = 0>
+template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                         const float* __restrict__ dO, const float* __restrict__ LSE,
@@ -429,23 +569,50 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     DkdvState<D, KB> st;
     FragOffsets<D> fo;
     fo.init(lane);
+    // 16x16x32 path (M16): its own state / offsets; the unused set is dead code
+    static_assert(!M16 || (KB == 1 && FA2_BWD_COAL), "16x16x32 dK/dV: 32 keys per wave, coalesced prologue");
+    DkdvState16<D> st16;
+    FragOffsets16<D> fo16;
+    const int g16 = lane >> 4;
+    if constexpr (M16) fo16.init(lane);
     (void)r;
 #if FA2_BWD_COAL
     static_assert(KPW * NW <= 4 * QT, "K / V block fits the Q/dO buffers");
     const int kblock0 = kblk * KPW * NW;
     stage_block<D, KPW * NW, NT>(smem, K + base, S, kblock0, kscale, tid);
     __syncthreads();
+    if constexpr (M16) {
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
+        for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-        for (int t = 0; t < D / 16; ++t) st.kf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
+            for (int ks = 0; ks < D / 32; ++ks) st16.kf[nb][ks] = fo16.rowop(smem, wave * KPW + 16 * nb, ks);
+    } else {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int t = 0; t < D / 16; ++t) st.kf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
+    }
     __syncthreads();
     stage_block<D, KPW * NW, NT>(smem, V + base, S, kblock0, 1.f, tid);
     __syncthreads();
+    if constexpr (M16) {
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
+        for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-        for (int t = 0; t < D / 16; ++t) st.vf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
+            for (int ks = 0; ks < D / 32; ++ks) st16.vf[nb][ks] = fo16.rowop(smem, wave * KPW + 16 * nb, ks);
+#pragma unroll
+        for (int md = 0; md < D / 16; ++md)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                st16.dka[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                st16.dva[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+    } else {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int t = 0; t < D / 16; ++t) st.vf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
+    }
     __syncthreads();
 #endif
 #pragma unroll
@@ -542,9 +709,14 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
             const bool more = !(ABL & 1) && it + 1 < nsteps;
             if (more) load_a(it + 1);
             FA2_STAMP(0);
-            dkdv_step<D, KB, ABL>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h, [&] {
-                if (more) load_b(it + 1);
-            });
+            if constexpr (M16)
+                dkdv_step16<D, ABL>(st16, smem, smem + TILE, rows[0][0], rows[0][1], fo16, g16, [&] {
+                    if (more) load_b(it + 1);
+                });
+            else
+                dkdv_step<D, KB, ABL>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h, [&] {
+                    if (more) load_b(it + 1);
+                });
             FA2_STAMP(1);
             if (more) store_step(smem + 2 * TILE, smem + 3 * TILE, 1);
             FA2_STAMP(2);
@@ -555,9 +727,14 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
             const bool more = !(ABL & 1) && it + 2 < nsteps;
             if (more) load_a(it + 2);
             FA2_STAMP(0);
-            dkdv_step<D, KB, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h, [&] {
-                if (more) load_b(it + 2);
-            });
+            if constexpr (M16)
+                dkdv_step16<D, ABL>(st16, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo16, g16, [&] {
+                    if (more) load_b(it + 2);
+                });
+            else
+                dkdv_step<D, KB, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h, [&] {
+                    if (more) load_b(it + 2);
+                });
             FA2_STAMP(1);
             if (more) store_step(smem, smem + TILE, 0);
             FA2_STAMP(2);
@@ -572,6 +749,11 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
 
     const float dscale = 1.f / __builtin_sqrtf((float)D);
 #if FA2_BWD_COAL
+    if constexpr (M16) {
+        store_block_rows16<D>(ostage[wave], st16.dka, dscale, dK + base + (long)key0 * D, S - key0, lane);
+        store_block_rows16<D>(ostage[wave], st16.dva, 1.f, dV + base + (long)key0 * D, S - key0, lane);
+        return;
+    }
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
         const int k0r = key0 + kb * 32;
@@ -993,7 +1175,7 @@ StampLog g_dkdv_stamps;
 #endif
 // waves per workgroup: 8 x 32 keys for D <= 64 (2 waves/SIMD fit in 256 VGPRs);
 // D = 128 needs more than 256 registers per lane, so 4 waves (1 per SIMD).
-template <int D, int NW, int KB = 1, int ABL = 0>
+template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false>
 hipError_t dkdv_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                        const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
     const long grid = (long)bh * ((S + 32 * KB * NW - 1) / (32 * KB * NW));
@@ -1007,16 +1189,16 @@ hipError_t dkdv_launch(const float* q, const float* k, const float* v, const flo
         (void)hipMalloc(&buf, n * sizeof(unsigned long long));
         cap = n;
     }
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, KB, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0,
-                       stream, q, k, v, dout, lse, delta, dk, dv, S, buf);
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, KB, ABL, M16>), dim3((unsigned)grid), dim3(64 * NW),
+                       0, stream, q, k, v, dout, lse, delta, dk, dv, S, buf);
     std::vector<unsigned long long> hst(n);
     (void)hipStreamSynchronize(stream);
     (void)hipMemcpy(hst.data(), buf, n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
     for (long i = 0; i < n; ++i) g_dkdv_stamps.sum[i % FA2_NSTAMP] += (double)hst[i] / (grid * NW);
     ++g_dkdv_stamps.launches;
 #else
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, KB, ABL>), dim3((unsigned)grid), dim3(64 * NW), 0,
-                       stream, q, k, v, dout, lse, delta, dk, dv, S);
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, KB, ABL, M16>), dim3((unsigned)grid), dim3(64 * NW),
+                       0, stream, q, k, v, dout, lse, delta, dk, dv, S);
 #endif
     return hipGetLastError();
 }
@@ -1046,7 +1228,13 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
         if (kbk == 2) {
             return dkdv_launch<D, 4, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
         }
-        if (nw == 8) return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        if (nw == 8) {
+            // FA2_TUNE_DKDV_MF: MFMA shape, 16 (16x16x32, default: +5 % at C3 -- fewer
+            // joules per FLOP under the power cap) or 32 (32x32x16)
+            if (tune_knob("DKDV_MF", 16) == 16)
+                return dkdv_launch<D, 8, 1, 0, true>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+            return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        }
     }
     if (nw == 2) return dkdv_launch<D, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
