@@ -826,10 +826,73 @@ __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, cons
             for (int s = 0; s < 2; ++s) st.dqa[b] = mfma(fo.trop(Ks, kb * 32 + 16 * s, b), dsf[kb][s], st.dqa[b]);
 }
 
+// ---- dQ on v_mfma_f32_16x16x32 (FA2_TUNE_DQ_MF=16), maps as in dkdv_step16:
+//   S^T / dP^T (m = key, n = query, k = d): A = K / V rows of the tile (row reads),
+//     B = Q / dO fragments in VGPRs; accumulators start at the lane's -lse2 / -delta.
+//   dQ^T (m = d, n = query, k = key): B = dS^T packed k-slot j <-> key
+//     16 (j >> 2) + 4g + (j & 3) of each 32-key half; A = K^T by transposed reads.
+template <int D>
+struct DqState16 {
+    f16x8 qf[2][D / 32], df[2][D / 32];  // [nb][ks]: Q (scaled) / dO[query 16 nb + (l&15)][d 32 ks + 8g ..]
+    f32x4 dqa[D / 16][2];                // [md][nb]
+    f32x4 nlse2[2], ndel[2];             // [nb]: splats of the lane's -lse2 / -delta
+};
+
+template <int D, bool MASK, typename Mid>
+__device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, const _Float16* Vs,
+                                          const FragOffsets16<D>& fo, int k0, int S, int g, Mid&& mid) {
+    f16x8 dsf[2][2];  // [32-key half kb][nb]
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        if (kb == 1) mid();  // the next tile's loads between the two 32-key halves (FA2_DQ_LP)
+        f32x4 sa[2][2], da[2][2];  // [mbl][nb]: keys k0 + 32 kb + 16 mbl + 4g + i
+#pragma unroll
+        for (int mbl = 0; mbl < 2; ++mbl)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                sa[mbl][nb] = st.nlse2[nb];
+                da[mbl][nb] = st.ndel[nb];
+            }
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks)
+#pragma unroll
+            for (int mbl = 0; mbl < 2; ++mbl) {
+                const f16x8 ka = fo.rowop(Ks, 32 * kb + 16 * mbl, ks), va = fo.rowop(Vs, 32 * kb + 16 * mbl, ks);
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    sa[mbl][nb] = mfma16(ka, st.qf[nb][ks], sa[mbl][nb]);
+                    da[mbl][nb] = mfma16(va, st.df[nb][ks], da[mbl][nb]);
+                }
+            }
+        if (MASK) {  // ragged last tile only
+#pragma unroll
+            for (int mbl = 0; mbl < 2; ++mbl)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (k0 + 32 * kb + 16 * mbl + 4 * g + i >= S) sa[mbl][nb][i] = -__builtin_inff();
+        }
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                dsf[kb][nb][j] = to_tile(fast_exp2(sa[j >> 2][nb][j & 3]) * da[j >> 2][nb][j & 3]);
+    }
+#pragma unroll
+    for (int md = 0; md < D / 16; ++md)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            const f16x8 a = fo.trop(Ks, 32 * kb, md);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) st.dqa[md][nb] = mfma16(a, dsf[kb][nb], st.dqa[md][nb]);
+        }
+}
+
 // DELTA: Δ is computed here (from O, fused into the dO prologue) and written to
 // `Delta` for the dK/dV kernel, which then runs after this one.
 // NKB 32-key blocks per K/V tile (1 for D = 128 at 8 waves: fewer registers).
-template <int D, int NW, bool DELTA = false, int NKB = 2>
+template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                       const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
@@ -856,11 +919,23 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     DqState<D> st;
     FragOffsets<D> fo;
     fo.init(lane);
+    static_assert(!M16 || (NKB == 2 && FA2_BWD_COAL), "16x16x32 dQ: 64-key tiles, coalesced prologue");
+    DqState16<D> st16;
+    FragOffsets16<D> fo16;
+    const int g16 = lane >> 4, i16 = lane & 15;
+    if constexpr (M16) fo16.init(lane);
 #if FA2_BWD_COAL
     stage_block<D, 32 * NW, NT>(smem, Q + base, S, qb * 32 * NW, qscale, tid);
     __syncthreads();
+    if constexpr (M16) {
 #pragma unroll
-    for (int t = 0; t < D / 16; ++t) st.qf[t] = fo.rowop(smem, wave * 32, t);
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int ks = 0; ks < D / 32; ++ks) st16.qf[nb][ks] = fo16.rowop(smem, wave * 32 + 16 * nb, ks);
+    } else {
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) st.qf[t] = fo.rowop(smem, wave * 32, t);
+    }
     __syncthreads();
     __shared__ float delta_blk[DELTA ? 32 * NW : 1];
     if (DELTA)
@@ -868,8 +943,15 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
                                           Delta + (long)bh * S, tid);
     else stage_block<D, 32 * NW, NT>(smem, dO + base, S, qb * 32 * NW, 1.f, tid);
     __syncthreads();
+    if constexpr (M16) {
 #pragma unroll
-    for (int t = 0; t < D / 16; ++t) st.df[t] = fo.rowop(smem, wave * 32, t);
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int ks = 0; ks < D / 32; ++ks) st16.df[nb][ks] = fo16.rowop(smem, wave * 32 + 16 * nb, ks);
+    } else {
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) st.df[t] = fo.rowop(smem, wave * 32, t);
+    }
     __syncthreads();
 #else
 #pragma unroll
@@ -895,6 +977,21 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     for (int b = 0; b < D / 32; ++b)
 #pragma unroll
         for (int i = 0; i < 16; ++i) st.dqa[b][i] = 0.f;
+    if constexpr (M16) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int qn = qb * 32 * NW + wave * 32 + 16 * nb + i16;
+            const bool ok = qn < S;
+            const float nl = ok ? -LSE[(long)bh * S + qn] * FA2B_LOG2E : -__builtin_inff();
+            const float nd = !ok ? 0.f : DELTA ? -delta_blk[wave * 32 + 16 * nb + i16] : -Delta[(long)bh * S + qn];
+            st16.nlse2[nb] = f32x4{nl, nl, nl, nl};
+            st16.ndel[nb] = f32x4{nd, nd, nd, nd};
+        }
+#pragma unroll
+        for (int md = 0; md < D / 16; ++md)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) st16.dqa[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
     // K/V staging by the first FA2_DQ_SW waves (all when 0), as in the dK/dV kernel
     constexpr int SW = (FA2_DQ_SW > 0 && FA2_DQ_SW < NW) ? FA2_DQ_SW : NW;
@@ -922,8 +1019,13 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
             auto mid = [&] {
                 if (more && FA2_DQ_LP) ld();
             };
-            if (j == last_ragged) dq_tile<D, true, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
-            else dq_tile<D, false, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
+            if constexpr (M16) {
+                if (j == last_ragged) dq_tile16<D, true>(st16, smem, smem + TILE, fo16, j * KT, S, g16, mid);
+                else dq_tile16<D, false>(st16, smem, smem + TILE, fo16, j * KT, S, g16, mid);
+            } else {
+                if (j == last_ragged) dq_tile<D, true, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
+                else dq_tile<D, false, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
+            }
             if (more) {
                 ks.store(smem + 2 * TILE, 1.f, tid);
                 vs.store(smem + 3 * TILE, 1.f, tid);
@@ -940,9 +1042,15 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
             auto mid = [&] {
                 if (more && FA2_DQ_LP) ld();
             };
-            if (j + 1 == last_ragged)
-                dq_tile<D, true, NKB>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
-            else dq_tile<D, false, NKB>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
+            if constexpr (M16) {
+                if (j + 1 == last_ragged)
+                    dq_tile16<D, true>(st16, smem + 2 * TILE, smem + 3 * TILE, fo16, (j + 1) * KT, S, g16, mid);
+                else dq_tile16<D, false>(st16, smem + 2 * TILE, smem + 3 * TILE, fo16, (j + 1) * KT, S, g16, mid);
+            } else {
+                if (j + 1 == last_ragged)
+                    dq_tile<D, true, NKB>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
+                else dq_tile<D, false, NKB>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
+            }
             if (more) {
                 ks.store(smem, 1.f, tid);
                 vs.store(smem + TILE, 1.f, tid);
@@ -954,8 +1062,12 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 #if FA2_BWD_COAL
     {
         const int q0w = qb * 32 * NW + wave * 32;
-        store_block_rows<D>(ostage[wave], st.dqa, 1.f / __builtin_sqrtf((float)D), dQ + base + (long)q0w * D, S - q0w,
-                            lane);
+        if constexpr (M16)
+            store_block_rows16<D>(ostage[wave], st16.dqa, 1.f / __builtin_sqrtf((float)D), dQ + base + (long)q0w * D,
+                                  S - q0w, lane);
+        else
+            store_block_rows<D>(ostage[wave], st.dqa, 1.f / __builtin_sqrtf((float)D), dQ + base + (long)q0w * D,
+                                S - q0w, lane);
     }
 #else
     if (qvalid) {
@@ -1239,19 +1351,19 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     if (nw == 2) return dkdv_launch<D, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
-template <int D, int NW, int NKB = 2>
+template <int D, int NW, int NKB = 2, bool M16 = false>
 hipError_t dq_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                      float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
     const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
 #if FA2_BWD_COAL
     if (o)
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0,
-                           stream, q, k, v, dout, lse, delta, dq, S, o);
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB, M16>), dim3((unsigned)grid),
+                           dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     else
 #endif
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0,
-                           stream, q, k, v, dout, lse, delta, dq, S, o);
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB, M16>), dim3((unsigned)grid),
+                           dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     return hipGetLastError();
 }
 template <int D>
@@ -1262,11 +1374,18 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     int nw = tune_knob("DQ_WAVES", 0);
     // (D = 128 at 8 waves spills even with 32-key tiles: Q, dO fragments, the -LSE / -Δ
     // seeds and the dQ accumulators alone are 160 VGPRs -- r01)
+    // (with 16x16x32 the seeds shrink to 8 VGPRs, but D = 128 at 8 waves still spills ~320)
     if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), D <= 64 ? 8 : 4, D <= 64 ? 2 : 4);
+    // FA2_TUNE_DQ_MF: MFMA shape, 16 (16x16x32, default: +2.4 % at C3) or 32 (32x32x16)
+    const bool m16 = tune_knob("DQ_MF", 16) == 16;
     if constexpr (D <= 64) {
-        if (nw == 8) return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        if (nw == 8) {
+            if (m16) return dq_launch<D, 8, 2, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+            return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        }
         if (nw == 2) return dq_launch<D, 2>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
     }
+    if (m16) return dq_launch<D, 4, 2, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
     return dq_launch<D, 4>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
 }
 }  // namespace
