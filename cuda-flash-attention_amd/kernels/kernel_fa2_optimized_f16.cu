@@ -63,10 +63,17 @@ __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
 }
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
 #else
 __device__ __forceinline__ _Float16 to_tile(float x) { return (_Float16)x; }
 __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 #endif
 
@@ -712,6 +719,261 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// forward on v_mfma_f32_16x16x32 (FA2_TUNE_FWD_MF=16).  Same algorithm as
+// fa2_fwd_f16_kernel (transposed S, -m seed, tile-sum overflow check); the wave's
+// 32 queries are two 16-query blocks nb, a KT-key tile is 2 NKB 16-key blocks mb.
+// Operand maps (lane l, g = l >> 4): A[m = l & 15][k = 8g + j], B[k = 8g + j][n = l & 15],
+// C[m = 4g + i][n = l & 15].
+//   S^T (m = key, n = query, k = d): A = K rows, B = Q fragments in VGPRs, seed -m.
+//   O^T (m = d, n = query, k = key): B = P^T packed k-slot j <-> key 16 (j >> 2) +
+//     4g + (j & 3) of each 32-key step; A = V^T by two 4-row transposed reads.
+// A query row is spread over lanes l, l ^ 16, l ^ 32, l ^ 48 (4 keys each per block):
+// the row max (slow path only) and the final row sum reduce over xor 16 and xor 32.
+// ---------------------------------------------------------------------------
+template <int D>
+struct FragOffsets16 {
+    int row[D / 32];
+    int tr[D / 16][2];
+    __device__ __forceinline__ void init(int lane) {
+        const int i = lane & 15, g = lane >> 4, q = i >> 2, p4 = i & 3;
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) row[ks] = tile_off<D>(i, 32 * ks + 8 * g);
+#pragma unroll
+        for (int md = 0; md < D / 16; ++md) {
+            tr[md][0] = tile_off<D>(4 * g + q, 16 * md + 4 * p4);
+            tr[md][1] = tile_off<D>(16 + 4 * g + q, 16 * md + 4 * p4);
+        }
+    }
+    __device__ __forceinline__ f16x8 rowop(const _Float16* tile, int r0, int ks) const {
+        return lds_row8(tile + row[ks] + r0 * D);
+    }
+    __device__ __forceinline__ f16x8 trop(const _Float16* tile, int r0, int md) const {
+        return cat4(lds_tr4(tile + tr[md][0] + r0 * D), lds_tr4(tile + tr[md][1] + r0 * D));
+    }
+};
+
+__device__ __forceinline__ float xor16_max(float x) { return fmaxf(x, __shfl_xor(x, 16)); }
+__device__ __forceinline__ float xor16_sum(float x) { return x + __shfl_xor(x, 16); }
+
+template <int D>
+struct Fwd16State {
+    f16x8 qf[2][D / 32];    // [nb][ks]: Q (scaled) [query 16 nb + (l&15)][d 32 ks + 8g ..]
+    f32x4 oacc[D / 16][2];  // [md][nb]: O^T [d 16 md + 4g + i][query]
+    f32x4 nm[2];            // [nb]: splat of -m
+    float m[2], l[2];       // [nb]: running max (log2 domain), this lane's partial row sum
+};
+
+template <int D, int NKB, bool MASK>
+__device__ __forceinline__ void fwd16_tile(Fwd16State<D>& st, const _Float16* Ks, const _Float16* Vs,
+                                           const FragOffsets16<D>& fo, int k0, int S, int g, bool first) {
+    constexpr int MB = 2 * NKB;  // 16-key blocks per tile
+    f32x4 sa[MB][2];
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+            const f16x8 ka = fo.rowop(Ks, 16 * mb, ks);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) sa[mb][nb] = mfma16(ka, st.qf[nb][ks], ks == 0 ? st.nm[nb] : sa[mb][nb]);
+        }
+    if (MASK) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (k0 + 16 * mb + 4 * g + i >= S) sa[mb][nb][i] = -__builtin_inff();
+    }
+    f16x8 pf[NKB][2];  // [32-key step][nb]
+    float ls[2];
+    auto expo = [&](float sh) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+            for (int kq = 0; kq < NKB; ++kq)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float pv = fast_exp2(sa[2 * kq + (j >> 2)][nb][j & 3] - sh);
+                    if (j & 1) a1 += pv;
+                    else a0 += pv;
+                    pf[kq][nb][j] = to_tile(pv);
+                }
+            ls[nb] = a0 + a1;
+        }
+    };
+    bool slow = first;
+    if (!first) {
+        expo(0.f);
+        const bool bad = !(ls[0] <= FA2_TILE_SUM_MAX) || !(ls[1] <= FA2_TILE_SUM_MAX);
+        slow = __any(bad);
+    }
+    auto pv_acc = [&]() {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) st.l[nb] += ls[nb];
+#pragma unroll
+        for (int md = 0; md < D / 16; ++md)
+#pragma unroll
+            for (int kq = 0; kq < NKB; ++kq) {
+                const f16x8 va = fo.trop(Vs, 32 * kq, md);
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) st.oacc[md][nb] = mfma16(va, pf[kq][nb], st.oacc[md][nb]);
+            }
+    };
+    if (slow) {
+        float dd[2];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            float mx = -__builtin_inff();
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sa[mb][nb][i]);
+            mx = xor32_max(xor16_max(mx));
+            const float d = first ? mx : fmaxf(mx, 0.f);
+            const float alpha = first ? 0.f : fast_exp2(-d);
+            st.m[nb] += d;
+            st.l[nb] *= alpha;
+#pragma unroll
+            for (int md = 0; md < D / 16; ++md) st.oacc[md][nb] *= alpha;
+            const float nmv = -st.m[nb];
+            st.nm[nb] = f32x4{nmv, nmv, nmv, nmv};
+            dd[nb] = d;
+        }
+        // p relative to the new m (sa holds s - m_old); two shifts as one expo pass
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+            for (int kq = 0; kq < NKB; ++kq)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float pv = fast_exp2(sa[2 * kq + (j >> 2)][nb][j & 3] - dd[nb]);
+                    if (j & 1) a1 += pv;
+                    else a0 += pv;
+                    pf[kq][nb][j] = to_tile(pv);
+                }
+            ls[nb] = a0 + a1;
+        }
+        pv_acc();
+    } else {
+        pv_acc();
+    }
+}
+
+template <int D, int NW, int NKB>
+__global__ void __launch_bounds__(64 * NW)
+fa2_fwd16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                 float* __restrict__ O, float* __restrict__ LSE, int S) {
+    constexpr int KT = 32 * NKB;
+    constexpr int NT = 64 * NW;
+    constexpr int TILE = KT * D;
+    constexpr int SMEM = (4 * TILE > 32 * NW * D) ? 4 * TILE : 32 * NW * D;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
+    __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+    const int nqb = (S + 32 * NW - 1) / (32 * NW);
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = bid / nqb, qb = bid - bh * nqb;
+    const long base = (long)bh * S * D;
+
+    FragOffsets16<D> fo;
+    fo.init(lane);
+    Fwd16State<D> st;
+    {
+        TileStager<D, 32 * NW, NT> qst;
+        qst.init(Q + base, S, tid);
+        qst.load(qb * 32 * NW);
+        qst.store(smem, FA2_LOG2E / __builtin_sqrtf((float)D), tid);
+        __syncthreads();
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int ks = 0; ks < D / 32; ++ks) st.qf[nb][ks] = fo.rowop(smem, wave * 32 + 16 * nb, ks);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+#pragma unroll
+        for (int md = 0; md < D / 16; ++md) st.oacc[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        st.nm[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        st.m[nb] = 0.f;
+        st.l[nb] = 0.f;
+    }
+    if (FA2_FWD_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    TileStager<D, KT, NT> ks, vs;
+    ks.init(K + base, S, tid);
+    vs.init(V + base, S, tid);
+    const int ntiles = (S + KT - 1) / KT;
+    const int last_ragged = (S % KT) ? ntiles - 1 : -1;
+    ks.load(0);
+    vs.load(0);
+    ks.store(smem, 1.f, tid);
+    vs.store(smem + TILE, 1.f, tid);
+    __syncthreads();
+    for (int j = 0; j < ntiles; j += 2) {
+        {
+            const bool more = j + 1 < ntiles;
+            if (more) {
+                ks.load((j + 1) * KT);
+                vs.load((j + 1) * KT);
+            }
+            if (j == last_ragged) fwd16_tile<D, NKB, true>(st, smem, smem + TILE, fo, j * KT, S, g, j == 0);
+            else fwd16_tile<D, NKB, false>(st, smem, smem + TILE, fo, j * KT, S, g, j == 0);
+            if (more) {
+                ks.store(smem + 2 * TILE, 1.f, tid);
+                vs.store(smem + 3 * TILE, 1.f, tid);
+            }
+            __syncthreads();
+        }
+        if (j + 1 < ntiles) {
+            const bool more = j + 2 < ntiles;
+            if (more) {
+                ks.load((j + 2) * KT);
+                vs.load((j + 2) * KT);
+            }
+            if (j + 1 == last_ragged)
+                fwd16_tile<D, NKB, true>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, g, false);
+            else fwd16_tile<D, NKB, false>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, g, false);
+            if (more) {
+                ks.store(smem, 1.f, tid);
+                vs.store(smem + TILE, 1.f, tid);
+            }
+            __syncthreads();
+        }
+    }
+    // O rows through the wave's LDS stage (row = query), LSE by the g == 0 lanes
+    const int q0w = qb * 32 * NW + wave * 32;
+    float inv[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+        const float lt = xor32_sum(xor16_sum(st.l[nb]));
+        inv[nb] = 1.f / lt;
+        const int qn = q0w + 16 * nb + i16;
+        if (g == 0 && qn < S) LSE[(long)bh * S + qn] = st.m[nb] * FA2_LN2 + __logf(lt);
+    }
+    float(*os)[36] = ostage[wave];
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b) {
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+                *reinterpret_cast<f32x4*>(&os[16 * nb + i16][16 * mh + 4 * g]) = st.oacc[2 * b + mh][nb] * inv[nb];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const int row = 8 * s4 + (lane >> 3), c4 = (lane & 7) * 4;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(&os[row][c4]);
+            if (q0w + row < S) *reinterpret_cast<f32x4*>(O + base + (long)(q0w + row) * D + 32 * b + c4) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
 // block 256, test_flash_attention2.py:278-281 / kernel_fa2_optimized_f16.cu:401),
 // fp16 tiles on MFMA like the library kernel.  A workgroup owns 32 query rows;
@@ -848,6 +1110,16 @@ static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v,
     return hipGetLastError();
 }
 
+template <int D, int NW, int NKB>
+static hipError_t fwd16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
+                               hipStream_t stream) {
+    const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16::fa2_fwd16_kernel<D, NW, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k, v,
+                       o, lse, S);
+    return hipGetLastError();
+}
+
 template <int D>
 static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
                                    hipStream_t stream) {
@@ -858,6 +1130,12 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     // FA2_TUNE_FWD_WAVES = 0 (default): auto_waves over the grid of 32-query wave units
     int nw = tune_knob("FWD_WAVES", 0);
     if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), 8);
+    // FA2_TUNE_FWD_MF: MFMA shape, 32 (32x32x16) or 16 (16x16x32, fa2_fwd16_kernel)
+    if (tune_knob("FWD_MF", 32) == 16) {
+        constexpr int NKB16 = D <= 64 ? 2 : 1;
+        if (nw == 8) return fwd16_launch<D, 8, NKB16>(q, k, v, o, lse, bh, S, stream);
+        if (nw == 4) return fwd16_launch<D, 4, NKB16>(q, k, v, o, lse, bh, S, stream);
+    }
     if constexpr (D <= 64) {
         if (nw == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
     } else {
