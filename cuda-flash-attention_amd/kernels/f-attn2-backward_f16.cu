@@ -79,17 +79,23 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 template <int D> struct Swz;
+// XOR swizzle of the 16-byte chunk index of LDS row r, searched (tools/lds_swizzle.py,
+// `swz_shipped`) to make ds_read_b128 row fragments and ds_read_b64_tr_b16 transposed
+// fragments bank-conflict-free for both the 32x32x16 and the 16x16x32 operand maps
+// (r01's first swizzle, searched for 32x32x16 only, left the 16x16x32 row reads 2-way:
+// 27-36 % extra LDS cycles in dK/dV and dQ).  Reads row bits 0..3 only (fragment
+// offsets are shifted by whole 16-row blocks).
 template <> struct Swz<32> {
-    static __device__ __forceinline__ int f(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) << 1); }
+    static __device__ __forceinline__ int f(int r) { return ((r >> 2) & 1) | ((((r >> 2) ^ (r >> 3)) & 1) << 1); }
 };
 template <> struct Swz<64> {
     static __device__ __forceinline__ int f(int r) {
-        return ((r >> 1) & 1) | (((r >> 2) & 1) << 1) | ((((r >> 1) ^ (r >> 3)) & 1) << 2);
+        return ((r >> 1) & 1) | ((((r >> 1) ^ (r >> 2)) & 1) << 1) | ((((r >> 1) ^ (r >> 3)) & 1) << 2);
     }
 };
 template <> struct Swz<128> {
     static __device__ __forceinline__ int f(int r) {
-        return (r & 1) | (((r >> 1) & 1) << 1) | (((r ^ (r >> 2)) & 1) << 2) | ((((r >> 1) ^ (r >> 3)) & 1) << 3);
+        return (r & 1) | (((r >> 1) & 1) << 1) | (((r ^ (r >> 2)) & 1) << 2) | (((r ^ (r >> 1) ^ (r >> 3)) & 1) << 3);
     }
 };
 template <int D>

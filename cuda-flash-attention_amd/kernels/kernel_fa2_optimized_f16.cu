@@ -80,9 +80,13 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // XOR swizzle of the 16-byte chunk index of LDS row r (fp16 rows of D halves).
-// Chosen by exhaustive search so that both access kinds used on a tile are
-// bank-conflict-free: ds_read_b128 row fragments (lane -> row) and
-// ds_read_b64_tr_b16 transposed fragments (4 rows x 32 cols per half-wave).
+// Chosen by search (tools/lds_swizzle.py, `swz_old`) so that the 32x32x16 access
+// kinds are bank-conflict-free: ds_read_b128 row fragments (lane -> row) and
+// ds_read_b64_tr_b16 transposed fragments.  The backward file's swizzle is also
+// conflict-free for the 16x16x32 maps its default kernels use; this forward's
+// default kernel is 32x32x16 (fa2_fwd16_kernel's row reads are 2-way here).  f reads
+// row bits 0..3 only: fragment offsets are computed once per lane and shifted by
+// whole 16-row blocks (FragOffsets*::rowop / trop add r0 * D).
 template <int D> struct Swz;
 template <> struct Swz<32> {
     static __device__ __forceinline__ int f(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) << 1); }

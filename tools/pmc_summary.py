@@ -24,7 +24,7 @@ def short(name):
     if not m:
         return None
     base = m.group(1)
-    t = re.search(r"<([0-9, ]+)>", name)
+    t = re.search(r"<([0-9a-z, ]+)>", name)
     return base + ("<" + t.group(1).replace(" ", "") + ">" if t else "")
 
 
