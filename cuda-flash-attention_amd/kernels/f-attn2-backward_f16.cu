@@ -1355,6 +1355,8 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
         }
     }
     if (nw == 2) return dkdv_launch<D, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+    // FA2_TUNE_DKDV_MF4: 16x16x32 at 4 waves too (default; +4 % at D = 128, +7 % at small D = 64 grids)
+    if (tune_knob("DKDV_MF4", 16) == 16) return dkdv_launch<D, 4, 1, 0, true>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
 template <int D, int NW, int NKB = 2, bool M16 = false>
