@@ -861,10 +861,12 @@ __device__ __forceinline__ void fwd16_tile(Fwd16State<D>& st, const _Float16* Ks
                 }
             ls[nb] = a0 + a1;
         }
-        pv_acc();
-    } else {
+        if (NKB == 2) pv_acc();
+    } else if (NKB == 2) {
         pv_acc();
     }
+    // 32-key tiles (D = 128 at 8 waves): one PV after the join (duplicated, it spills)
+    if (NKB != 2) pv_acc();
 }
 
 template <int D, int NW, int NKB>
