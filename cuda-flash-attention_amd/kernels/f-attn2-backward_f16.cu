@@ -844,13 +844,13 @@ struct DqState16 {
     f32x4 nlse2[2], ndel[2];             // [nb]: splats of the lane's -lse2 / -delta
 };
 
-template <int D, bool MASK, typename Mid>
+template <int D, bool MASK, int NKB, typename Mid>
 __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, const _Float16* Vs,
                                           const FragOffsets16<D>& fo, int k0, int S, int g, Mid&& mid) {
-    f16x8 dsf[2][2];  // [32-key half kb][nb]
+    f16x8 dsf[NKB][2];  // [32-key half kb][nb]
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-        if (kb == 1) mid();  // the next tile's loads between the two 32-key halves (FA2_DQ_LP)
+    for (int kb = 0; kb < NKB; ++kb) {
+        if (NKB > 1 && kb == 1) mid();  // the next tile's loads between the two 32-key halves (FA2_DQ_LP)
         f32x4 sa[2][2], da[2][2];  // [mbl][nb]: keys k0 + 32 kb + 16 mbl + 4g + i
 #pragma unroll
         for (int mbl = 0; mbl < 2; ++mbl)
@@ -879,6 +879,7 @@ __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, 
                     for (int i = 0; i < 4; ++i)
                         if (k0 + 32 * kb + 16 * mbl + 4 * g + i >= S) sa[mbl][nb][i] = -__builtin_inff();
         }
+        if (NKB == 1) mid();  // 32-key tiles: after the tile's S / dP MFMAs
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
@@ -888,7 +889,7 @@ __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, 
 #pragma unroll
     for (int md = 0; md < D / 16; ++md)
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
+        for (int kb = 0; kb < NKB; ++kb) {
             const f16x8 a = fo.trop(Ks, 32 * kb, md);
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) st.dqa[md][nb] = mfma16(a, dsf[kb][nb], st.dqa[md][nb]);
@@ -925,7 +926,7 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     DqState<D> st;
     FragOffsets<D> fo;
     fo.init(lane);
-    static_assert(!M16 || (NKB == 2 && FA2_BWD_COAL), "16x16x32 dQ: 64-key tiles, coalesced prologue");
+    static_assert(!M16 || FA2_BWD_COAL, "16x16x32 dQ: coalesced prologue");
     DqState16<D> st16;
     FragOffsets16<D> fo16;
     const int g16 = lane >> 4, i16 = lane & 15;
@@ -1026,8 +1027,8 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
                 if (more && FA2_DQ_LP) ld();
             };
             if constexpr (M16) {
-                if (j == last_ragged) dq_tile16<D, true>(st16, smem, smem + TILE, fo16, j * KT, S, g16, mid);
-                else dq_tile16<D, false>(st16, smem, smem + TILE, fo16, j * KT, S, g16, mid);
+                if (j == last_ragged) dq_tile16<D, true, NKB>(st16, smem, smem + TILE, fo16, j * KT, S, g16, mid);
+                else dq_tile16<D, false, NKB>(st16, smem, smem + TILE, fo16, j * KT, S, g16, mid);
             } else {
                 if (j == last_ragged) dq_tile<D, true, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
                 else dq_tile<D, false, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
@@ -1050,8 +1051,9 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
             };
             if constexpr (M16) {
                 if (j + 1 == last_ragged)
-                    dq_tile16<D, true>(st16, smem + 2 * TILE, smem + 3 * TILE, fo16, (j + 1) * KT, S, g16, mid);
-                else dq_tile16<D, false>(st16, smem + 2 * TILE, smem + 3 * TILE, fo16, (j + 1) * KT, S, g16, mid);
+                    dq_tile16<D, true, NKB>(st16, smem + 2 * TILE, smem + 3 * TILE, fo16, (j + 1) * KT, S, g16, mid);
+                else dq_tile16<D, false, NKB>(st16, smem + 2 * TILE, smem + 3 * TILE, fo16, (j + 1) * KT, S, g16,
+                                              mid);
             } else {
                 if (j + 1 == last_ragged)
                     dq_tile<D, true, NKB>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
@@ -1382,7 +1384,8 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     int nw = tune_knob("DQ_WAVES", 0);
     // (D = 128 at 8 waves spills even with 32-key tiles: Q, dO fragments, the -LSE / -Δ
     // seeds and the dQ accumulators alone are 160 VGPRs -- r01)
-    // (with 16x16x32 the seeds shrink to 8 VGPRs, but D = 128 at 8 waves still spills ~320)
+    // (D = 128 at 8 waves on 16x16x32 with 32-key tiles still spills ~70 VGPRs inside the
+    // loop: Q, dO fragments and the dQ accumulators alone take 128)
     if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), D <= 64 ? 8 : 4, D <= 64 ? 2 : 4);
     // FA2_TUNE_DQ_MF: MFMA shape, 16 (16x16x32, default: +2.4 % at C3) or 32 (32x32x16)
     const bool m16 = tune_knob("DQ_MF", 16) == 16;
