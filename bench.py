@@ -97,9 +97,13 @@ def cpu_baseline(S, D, sample_heads=None):
             "sample": f"{heads} heads x (S={S}, D={D}) fp32 fwd+bwd, oracle/fa2_oracle.c, {dt:.2f} s"}
 
 
-def time_config(fa2amd, torch, dev, B, H, S, D, prec, fwd_only, iters=50, warmup=3, warmup_ms=250.0):
+def time_config(fa2amd, torch, dev, B, H, S, D, prec, fwd_only, iters=50, warmup=3, warmup_ms=250.0, dist=None,
+                total_heads=None):
     """Mean ms of fwd (+ bwd) on one synthetic config (harness distribution), events on
-    the current stream; returns (ms, tflops, gbps) with the algorithmic counts."""
+    the current stream; returns (ms, tflops, gbps) with the algorithmic counts.  With
+    `dist` (multi-GPU sweep): each rank runs its own B x H slice, the region is
+    bracketed by barriers, ms is the max over ranks and the rates count
+    `total_heads` heads."""
     gen = torch.Generator().manual_seed(7)
     q, k, v = (torch.rand(B, H, S, D, generator=gen).to(dev) for _ in range(3))
     do = torch.ones_like(q)
@@ -119,15 +123,55 @@ def time_config(fa2amd, torch, dev, B, H, S, D, prec, fwd_only, iters=50, warmup
             torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+        torch.cuda.synchronize(dev)
     e0.record()
     for _ in range(iters):
         once()
     e1.record()
     e1.synchronize()
     ms = e0.elapsed_time(e1) / iters
-    flops = (4.0 if fwd_only else 14.0) * B * H * S * S * D
-    nbytes = (16.0 * S * D + 4.0 * S if fwd_only else 48.0 * S * D + 8.0 * S) * B * H
+    if dist is not None:
+        ms = all_max(torch, dist, dev, ms)
+    heads = total_heads or B * H
+    flops = (4.0 if fwd_only else 14.0) * heads * S * S * D
+    nbytes = (16.0 * S * D + 4.0 * S if fwd_only else 48.0 * S * D + 8.0 * S) * heads
     return ms, flops / ms / 1e9, nbytes / ms / 1e6
+
+
+def all_max(torch, dist, dev, x):
+    """max over ranks of a host float (RCCL needs a device tensor, gloo a host one)"""
+    t = torch.tensor([x], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def roof_entry(ms, tf, gbps, S, fwd_only):
+    """A sweep point against its binding roofline: algorithmic intensity (fwd S/4,
+    fwd+bwd 14 S / 48 FLOP/B at fp32 I/O) below the fp16 MFMA ridge (peak FLOP/s over
+    HBM B/s) means HBM-bound."""
+    intensity = (S / 4.0) if fwd_only else (14.0 * S / 48.0)
+    ridge = MFMA_F16_PEAK_TFLOPS * 1e3 / HBM_PEAK_GBPS
+    fm, fh = tf / MFMA_F16_PEAK_TFLOPS, gbps / HBM_PEAK_GBPS
+    bound = "hbm" if intensity < ridge else "mfma"
+    return {"ms": round(ms, 4), "tflops": round(tf, 2), "hbm_gbps": round(gbps, 1), "frac_mfma": round(fm, 4),
+            "frac_hbm": round(fh, 4), "bound": bound, "frac": round(fh if bound == "hbm" else fm, 4)}
+
+
+SWEEP_S = (512, 1024, 2048, 4096)
+
+
+def sweep_sharded(fa2amd, torch, dev, dist, world, rank):
+    """north_star's sweep, B2_H8_S{512..4096}_D64 fwd+bwd, with its 16 heads sharded
+    over the ranks (contiguous B x H slices, no collective on the data path): the
+    1/2/4/8-GPU points the north star asks for."""
+    first, heads = fa2amd.shard_range(16, world, rank)
+    out = {}
+    for S in SWEEP_S:
+        ms, tf, gbps = time_config(fa2amd, torch, dev, 1, heads, S, 64, "fp16", False, dist=dist, total_heads=16)
+        out[str(S)] = roof_entry(ms, tf, gbps, S, False)
+    return out
 
 
 def torch_sdpa_cpu(S, D, heads):
@@ -150,11 +194,9 @@ def torch_sdpa_cpu(S, D, heads):
 def extras(fa2amd, torch, dev):
     """north_star's sweep and BASELINE.json's other GPU configs, each against its roofline."""
     out = {"sweep_B2_H8_D64_fp16_fwdbwd": {}}
-    for S in (512, 1024, 2048, 4096):
+    for S in SWEEP_S:
         ms, tf, gbps = time_config(fa2amd, torch, dev, 2, 8, S, 64, "fp16", False)
-        out["sweep_B2_H8_D64_fp16_fwdbwd"][str(S)] = {"ms": round(ms, 4), "tflops": round(tf, 2),
-                                                      "hbm_gbps": round(gbps, 1),
-                                                      "frac_mfma": round(tf / MFMA_F16_PEAK_TFLOPS, 4)}
+        out["sweep_B2_H8_D64_fp16_fwdbwd"][str(S)] = roof_entry(ms, tf, gbps, S, False)
     ms, tf, gbps = time_config(fa2amd, torch, dev, 8, 16, 4096, 128, "fp16", True, iters=20)
     out["c4_B8_H16_S4096_D128_fp16_fwd"] = {"ms": round(ms, 4), "tflops": round(tf, 2), "hbm_gbps": round(gbps, 1),
                                             "frac_mfma": round(tf / MFMA_F16_PEAK_TFLOPS, 4),
@@ -190,9 +232,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FA2_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- rehearses the N > 1 path
+    # (barriers, max over ranks, sharded sweep) on a one-GPU box; never used for numbers
+    rehearse = os.environ.get("FA2_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -263,9 +313,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = all_max(torch, dist, dev, elapsed)
 
     # timed region 2 -> roofline: the same K steps with HIP events around every kernel
     # on its stream; these per-launch durations are the isolated ones rocprofv3's
@@ -303,6 +351,8 @@ def main():
     extra = None
     if rank == 0 and world == 1 and not args.no_extras:
         extra = extras(fa2amd, torch, dev)
+    elif world > 1 and not args.no_extras:
+        extra = {f"sweep_B2_H8_D64_fp16_fwdbwd_sharded{world}": sweep_sharded(fa2amd, torch, dev, dist, world, rank)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(S, D)

@@ -406,9 +406,11 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
         tprev = t_;                                                                               \
     } while (0)
 #define FA2_STAMP_ARG , unsigned long long* __restrict__ stamps
+#define FA2_STAMPS_ON 1
 #else
 #define FA2_STAMP(k)
 #define FA2_STAMP_ARG
+#define FA2_STAMPS_ON 0
 #endif
 
 // ---- dK, dV on v_mfma_f32_16x16x32 (FA2_TUNE_DKDV_MF=16) ------------------------
@@ -442,6 +444,16 @@ struct FragOffsets16 {
         for (int md = 0; md < D / 16; ++md) {
             tr[md][0] = tile_off<D>(4 * g + q, 16 * md + 4 * p4);
             tr[md][1] = tile_off<D>(16 + 4 * g + q, 16 * md + 4 * p4);
+        }
+    }
+    // move every offset by o halves (a wave's fixed tile inside a multi-tile image)
+    __device__ __forceinline__ void shift(int o) {
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) row[ks] += o;
+#pragma unroll
+        for (int md = 0; md < D / 16; ++md) {
+            tr[md][0] += o;
+            tr[md][1] += o;
         }
     }
     // A operand: rows r0 + (l & 15), k-step ks over columns
@@ -544,9 +556,13 @@ __device__ __forceinline__ void store_block_rows16(float (*os)[36], const f32x4 
     }
 }
 
-// KB x 32 keys per wave, NW waves: grid BH * ceil(S / (32*KB*NW)), block 64*NW.
+// KB x 32 keys per wave, NW waves: grid BH * ceil(S / (32*KB*NK)), block 64*NW.
 // ABL: timing ablations (see dkdv_step; plus 1 = no staging in the loop, 4 = no barrier)
-template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false>
+// QS > 1 (small grids; 16x16x32 path): the query range is split over QS wave groups
+// of NK = NW / QS waves.  Wave w keeps keys of slot w % NK and takes query tiles
+// it·QS + w / NK; each step stages QS tiles.  After the loop the groups' dKᵀ / dVᵀ
+// are summed in LDS in group order (deterministic) and group 0 stores.
+template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false, int QS = 1>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                         const float* __restrict__ dO, const float* __restrict__ LSE,
@@ -556,20 +572,27 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     constexpr int NT = 64 * NW;
     constexpr int TILE = QT * D;
     constexpr int KPW = 32 * KB;  // keys per wave
-    // [buf][Q | dO] fp16 tiles, then [buf][-lse2 | -delta] fp32 rows
-    __shared__ __attribute__((aligned(16))) _Float16 smem[2 * 2 * TILE];
-    __shared__ __attribute__((aligned(16))) float rows[2][2][QT];
+    static_assert(QS == 1 || (M16 && 2 * QS <= NW && !FA2_STAMPS_ON), "query split: 16x16x32, 2 QS row waves");
+    constexpr int NK = NW / QS;  // key waves (QS > 1: waves w, w + NK, ... share keys)
+    // query-split merge records: per wave of groups 1..QS-1, dKᵀ and dVᵀ (D floats per lane)
+    constexpr int MERGE = QS > 1 ? 2 * (QS - 1) * NK * D * 64 : 0;  // in halves
+    constexpr int SMEM = 2 * 2 * QS * TILE > MERGE ? 2 * 2 * QS * TILE : MERGE;
+    // [buf][Q | dO][QS] fp16 tiles, then [buf][-lse2 | -delta][QS] fp32 rows
+    __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
+    __shared__ __attribute__((aligned(16))) float rows[2][2][QS * QT];
 #if FA2_BWD_COAL
-    __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];  // per-wave result stage
+    __shared__ __attribute__((aligned(16))) float ostage[NK][32][36];  // per-wave result stage
 #endif
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int nkb = (S + KPW * NW - 1) / (KPW * NW);
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = QS > 1 ? (tid >> 6) % NK : tid >> 6;  // key slot of the wave
+    const int qg = QS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NK) : 0;  // query group
+    const int nkb = (S + KPW * NK - 1) / (KPW * NK);
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = bid / nkb, kblk = bid - bh * nkb;
     const long base = (long)bh * S * D;
     const long rbase = (long)bh * S;
-    const int key0 = kblk * KPW * NW + wave * KPW;  // this wave's first key
+    const int key0 = kblk * KPW * NK + wave * KPW;  // this wave's first key
     const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
 
     DkdvState<D, KB> st;
@@ -583,9 +606,9 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     if constexpr (M16) fo16.init(lane);
     (void)r;
 #if FA2_BWD_COAL
-    static_assert(KPW * NW <= 4 * QT, "K / V block fits the Q/dO buffers");
-    const int kblock0 = kblk * KPW * NW;
-    stage_block<D, KPW * NW, NT>(smem, K + base, S, kblock0, kscale, tid);
+    static_assert(KPW * NK <= 4 * QT, "K / V block fits the Q/dO buffers");
+    const int kblock0 = kblk * KPW * NK;
+    stage_block<D, KPW * NK, NT>(smem, K + base, S, kblock0, kscale, tid);
     __syncthreads();
     if constexpr (M16) {
 #pragma unroll
@@ -599,7 +622,7 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
             for (int t = 0; t < D / 16; ++t) st.kf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
     }
     __syncthreads();
-    stage_block<D, KPW * NW, NT>(smem, V + base, S, kblock0, 1.f, tid);
+    stage_block<D, KPW * NK, NT>(smem, V + base, S, kblock0, 1.f, tid);
     __syncthreads();
     if constexpr (M16) {
 #pragma unroll
@@ -646,8 +669,9 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     // so the staging work goes to the first half.
     constexpr int SW = (FA2_DKDV_SW > 0 && FA2_DKDV_SW < NW) ? FA2_DKDV_SW : NW;
     constexpr int NS = 64 * SW;
-    const bool stg = __builtin_amdgcn_readfirstlane(wave) < SW;
-    TileStager<D, QT, NS> qs, dos;
+    const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool stg = wave_u < SW;
+    TileStager<D, QT * QS, NS> qs, dos;
     qs.init(Q + base, S, tid);
     dos.init(dO + base, S, tid);
     // Row constants of the staged step: wave 0 carries LSE, wave 1 carries Delta
@@ -655,39 +679,42 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     // read 0) and only scaled / negated / masked at store time, so nothing waits on
     // the load before the step's MFMAs (a guarded global load there made the
     // compiler drain vmcnt -- the K/V staging loads too -- at every step start).
+    // (QS > 1: waves 0..QS-1 carry the LSE rows of the step's QS tiles, waves
+    // QS..2QS-1 the Delta rows)
     static_assert(QT == 64, "one wave per row vector");
-    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     if (FA2_DKDV_PRIO && NW == 8 && wave_u >= NW / 2) __builtin_amdgcn_s_setprio(1);
     const __amdgpu_buffer_rsrc_t rs_lse = head_rsrc(LSE + rbase, S, 1);
     const __amdgpu_buffer_rsrc_t rs_del = head_rsrc(Delta + rbase, S, 1);
     float rowraw = 0.f;
     int rowq = 0;
+    const int rw = wave_u % QS;  // which of the step's tiles this wave's row vector is
     auto load_rows = [&](int q0) {
+        q0 += rw * QT;
         rowq = q0 + lane;
-        if (wave_u == 0) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
-        else if (wave_u == 1) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_del, lane * 4, q0 * 4, 0));
+        if (wave_u < QS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
+        else if (wave_u < 2 * QS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_del, lane * 4, q0 * 4, 0));
     };
     auto store_rows = [&](int buf) {
         // stored negated: they are the initial accumulators of S and dP
-        if (wave_u == 0) rows[buf][0][lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
-        else if (wave_u == 1) rows[buf][1][lane] = -rowraw;
+        if (wave_u < QS) rows[buf][0][rw * QT + lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
+        else if (wave_u < 2 * QS) rows[buf][1][rw * QT + lane] = -rowraw;
     };
     // where the next step's global loads are issued (all eight waves issuing them at
     // once right after the barrier queue on the texture unit): FA2_DKDV_LP
     // 0 = all at the step start, 1 = all between the two query blocks, 2 = Q at the
     // start and dO + row constants between the blocks
     auto load_a = [&](int it) {
-        if ((FA2_DKDV_LP == 0 || FA2_DKDV_LP == 2) && stg) qs.load(it * QT);
+        if ((FA2_DKDV_LP == 0 || FA2_DKDV_LP == 2) && stg) qs.load(it * QS * QT);
         if (FA2_DKDV_LP == 0) {
-            if (stg) dos.load(it * QT);
-            load_rows(it * QT);
+            if (stg) dos.load(it * QS * QT);
+            load_rows(it * QS * QT);
         }
     };
     auto load_b = [&](int it) {
-        if (FA2_DKDV_LP == 1 && stg) qs.load(it * QT);
+        if (FA2_DKDV_LP == 1 && stg) qs.load(it * QS * QT);
         if (FA2_DKDV_LP != 0) {
-            if (stg) dos.load(it * QT);
-            load_rows(it * QT);
+            if (stg) dos.load(it * QS * QT);
+            load_rows(it * QS * QT);
         }
     };
     auto store_step = [&](_Float16* qdst, _Float16* ddst, int rbuf) {
@@ -697,14 +724,18 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
         }
         store_rows(rbuf);
     };
-    const int nsteps = (S + QT - 1) / QT;
+    const int nqt = (S + QT - 1) / QT;  // query tiles
+    const int nsteps = (nqt + QS - 1) / QS;
     if (stg) {
         qs.load(0);
         dos.load(0);
     }
     load_rows(0);
-    store_step(smem, smem + TILE, 0);
+    store_step(smem, smem + QS * TILE, 0);
     __syncthreads();
+    // the group's tile within each staged image: folded into the per-lane offsets
+    if (QS > 1) fo16.shift(qg * TILE);
+    const int rq = qg * QT;  // the group's row constants
 
 #ifdef FA2_STAMPS
     unsigned long long stv[FA2_NSTAMP] = {0, 0, 0, 0, 0}, tprev;
@@ -713,36 +744,40 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     for (int it = 0; it < nsteps; it += 2) {
         {
             const bool more = !(ABL & 1) && it + 1 < nsteps;
+            const bool live = QS == 1 || it * QS + qg < nqt;  // wave-uniform
             if (more) load_a(it + 1);
             FA2_STAMP(0);
-            if constexpr (M16)
-                dkdv_step16<D, ABL>(st16, smem, smem + TILE, rows[0][0], rows[0][1], fo16, g16, [&] {
-                    if (more) load_b(it + 1);
-                });
-            else
-                dkdv_step<D, KB, ABL>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h, [&] {
-                    if (more) load_b(it + 1);
-                });
+            auto mid = [&] {
+                if (more) load_b(it + 1);
+            };
+            if constexpr (M16) {
+                if (live) dkdv_step16<D, ABL>(st16, smem, smem + QS * TILE, rows[0][0] + rq, rows[0][1] + rq, fo16, g16, mid);
+                else mid();
+            } else
+                dkdv_step<D, KB, ABL>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h, mid);
             FA2_STAMP(1);
-            if (more) store_step(smem + 2 * TILE, smem + 3 * TILE, 1);
+            if (more) store_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, 1);
             FA2_STAMP(2);
             if (!(ABL & 4)) __syncthreads();
             FA2_STAMP(3);
         }
         if (it + 1 < nsteps) {
             const bool more = !(ABL & 1) && it + 2 < nsteps;
+            const bool live = QS == 1 || (it + 1) * QS + qg < nqt;
             if (more) load_a(it + 2);
             FA2_STAMP(0);
-            if constexpr (M16)
-                dkdv_step16<D, ABL>(st16, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo16, g16, [&] {
-                    if (more) load_b(it + 2);
-                });
-            else
-                dkdv_step<D, KB, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h, [&] {
-                    if (more) load_b(it + 2);
-                });
+            auto mid = [&] {
+                if (more) load_b(it + 2);
+            };
+            if constexpr (M16) {
+                if (live)
+                    dkdv_step16<D, ABL>(st16, smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0] + rq, rows[1][1] + rq,
+                                        fo16, g16, mid);
+                else mid();
+            } else
+                dkdv_step<D, KB, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h, mid);
             FA2_STAMP(1);
-            if (more) store_step(smem, smem + TILE, 0);
+            if (more) store_step(smem, smem + QS * TILE, 0);
             FA2_STAMP(2);
             if (!(ABL & 4)) __syncthreads();
             FA2_STAMP(3);
@@ -753,6 +788,38 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
         for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blockIdx.x * NW + wave) * FA2_NSTAMP + k] = stv[k];
 #endif
 
+    if constexpr (QS > 1) {
+        // query-split merge (the loop ended on a barrier: the tile buffers are free);
+        // lane-linear records, summed in group order
+        float* mg = reinterpret_cast<float*>(smem);
+        if (qg > 0) {
+            float* rec = mg + ((qg - 1) * NK + wave) * D * 64;
+#pragma unroll
+            for (int md = 0; md < D / 16; ++md)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        rec[((md * 2 + nb) * 4 + i) * 64 + lane] = st16.dka[md][nb][i];
+                        rec[(D / 2 + (md * 2 + nb) * 4 + i) * 64 + lane] = st16.dva[md][nb][i];
+                    }
+        }
+        __syncthreads();
+        if (qg > 0) return;  // no workgroup barrier follows
+#pragma unroll
+        for (int g = 1; g < QS; ++g) {
+            const float* rec = mg + ((g - 1) * NK + wave) * D * 64;
+#pragma unroll
+            for (int md = 0; md < D / 16; ++md)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        st16.dka[md][nb][i] += rec[((md * 2 + nb) * 4 + i) * 64 + lane];
+                        st16.dva[md][nb][i] += rec[(D / 2 + (md * 2 + nb) * 4 + i) * 64 + lane];
+                    }
+        }
+    }
     const float dscale = 1.f / __builtin_sqrtf((float)D);
 #if FA2_BWD_COAL
     if constexpr (M16) {
@@ -899,7 +966,11 @@ __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, 
 // DELTA: Δ is computed here (from O, fused into the dO prologue) and written to
 // `Delta` for the dK/dV kernel, which then runs after this one.
 // NKB 32-key blocks per K/V tile (1 for D = 128 at 8 waves: fewer registers).
-template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false>
+// KS > 1 (small grids; 16x16x32 path): the key range is split over KS wave groups of
+// NQ = NW / KS waves.  Wave w keeps query rows of slot w % NQ and takes K/V tiles
+// j·KS + w / NQ; each step stages KS tiles.  After the loop the groups' dQᵀ are
+// summed in LDS in group order (deterministic) and group 0 stores.
+template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                       const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
@@ -907,19 +978,26 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     constexpr int KT = 32 * NKB;
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
-    // [buf][K | V] tiles; at least one Q block (coalesced prologue) in size
-    constexpr int SMEM = (4 * TILE > 32 * NW * D) ? 4 * TILE : 32 * NW * D;
+    static_assert(KS == 1 || (M16 && NW % KS == 0), "key split: 16x16x32");
+    constexpr int NQ = NW / KS;  // query waves (KS > 1: waves w, w + NQ, ... share rows)
+    // key-split merge records: per wave of groups 1..KS-1, dQᵀ (D / 2 floats per lane)
+    constexpr int MERGE = KS > 1 ? 2 * (KS - 1) * NQ * (D / 2) * 64 : 0;  // in halves
+    // [buf][K | V][KS] tiles; at least one Q block (coalesced prologue) and the merge
+    constexpr int SMEM0 = (4 * KS * TILE > 32 * NQ * D) ? 4 * KS * TILE : 32 * NQ * D;
+    constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;
     __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
 #if FA2_BWD_COAL
-    __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];  // per-wave dQ stage
+    __shared__ __attribute__((aligned(16))) float ostage[NQ][32][36];  // per-wave dQ stage
 #endif
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int nqb = (S + 32 * NW - 1) / (32 * NW);
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = KS > 1 ? (tid >> 6) % NQ : tid >> 6;  // query slot of the wave
+    const int kg = KS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NQ) : 0;  // key group
+    const int nqb = (S + 32 * NQ - 1) / (32 * NQ);
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = bid / nqb, qb = bid - bh * nqb;
     const long base = (long)bh * S * D;
-    const int q = qb * 32 * NW + wave * 32 + r;
+    const int q = qb * 32 * NQ + wave * 32 + r;
     const bool qvalid = q < S;
     const float qscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
 
@@ -932,7 +1010,7 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     const int g16 = lane >> 4, i16 = lane & 15;
     if constexpr (M16) fo16.init(lane);
 #if FA2_BWD_COAL
-    stage_block<D, 32 * NW, NT>(smem, Q + base, S, qb * 32 * NW, qscale, tid);
+    stage_block<D, 32 * NQ, NT>(smem, Q + base, S, qb * 32 * NQ, qscale, tid);
     __syncthreads();
     if constexpr (M16) {
 #pragma unroll
@@ -944,11 +1022,11 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
         for (int t = 0; t < D / 16; ++t) st.qf[t] = fo.rowop(smem, wave * 32, t);
     }
     __syncthreads();
-    __shared__ float delta_blk[DELTA ? 32 * NW : 1];
+    __shared__ float delta_blk[DELTA ? 32 * NQ : 1];
     if (DELTA)
-        stage_block_delta<D, 32 * NW, NT>(smem, dO + base, O + base, S, qb * 32 * NW, delta_blk,
+        stage_block_delta<D, 32 * NQ, NT>(smem, dO + base, O + base, S, qb * 32 * NQ, delta_blk,
                                           Delta + (long)bh * S, tid);
-    else stage_block<D, 32 * NW, NT>(smem, dO + base, S, qb * 32 * NW, 1.f, tid);
+    else stage_block<D, 32 * NQ, NT>(smem, dO + base, S, qb * 32 * NQ, 1.f, tid);
     __syncthreads();
     if constexpr (M16) {
 #pragma unroll
@@ -987,7 +1065,7 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     if constexpr (M16) {
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
-            const int qn = qb * 32 * NW + wave * 32 + 16 * nb + i16;
+            const int qn = qb * 32 * NQ + wave * 32 + 16 * nb + i16;
             const bool ok = qn < S;
             const float nl = ok ? -LSE[(long)bh * S + qn] * FA2B_LOG2E : -__builtin_inff();
             const float nd = !ok ? 0.f : DELTA ? -delta_blk[wave * 32 + 16 * nb + i16] : -Delta[(long)bh * S + qn];
@@ -1002,57 +1080,66 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 
     // K/V staging by the first FA2_DQ_SW waves (all when 0), as in the dK/dV kernel
     constexpr int SW = (FA2_DQ_SW > 0 && FA2_DQ_SW < NW) ? FA2_DQ_SW : NW;
-    TileStager<D, KT, 64 * SW> ks, vs;
+    TileStager<D, KT * KS, 64 * SW> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
-    ks.on = vs.on = __builtin_amdgcn_readfirstlane(wave) < SW;
-    if (FA2_DQ_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    ks.on = vs.on = __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
+    if (FA2_DQ_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(tid >> 6) >= NW / 2) __builtin_amdgcn_s_setprio(1);
     const int ntiles = (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
+    const int nsteps = (ntiles + KS - 1) / KS;
     ks.load(0);
     vs.load(0);
     ks.store(smem, 1.f, tid);
-    vs.store(smem + TILE, 1.f, tid);
+    vs.store(smem + KS * TILE, 1.f, tid);
     __syncthreads();
+    // the group's tile within each staged image: folded into the per-lane offsets
+    if (KS > 1) fo16.shift(kg * TILE);
 
-    for (int j = 0; j < ntiles; j += 2) {
+    for (int j = 0; j < nsteps; j += 2) {
         {
-            const bool more = j + 1 < ntiles;
+            const bool more = j + 1 < nsteps;
+            const int jj = j * KS + kg;             // this wave's tile
+            const bool live = KS == 1 || jj < ntiles;  // wave-uniform
             auto ld = [&] {
-                ks.load((j + 1) * KT);
-                vs.load((j + 1) * KT);
+                ks.load((j + 1) * KS * KT);
+                vs.load((j + 1) * KS * KT);
             };
             if (more && !FA2_DQ_LP) ld();
             auto mid = [&] {
                 if (more && FA2_DQ_LP) ld();
             };
             if constexpr (M16) {
-                if (j == last_ragged) dq_tile16<D, true, NKB>(st16, smem, smem + TILE, fo16, j * KT, S, g16, mid);
-                else dq_tile16<D, false, NKB>(st16, smem, smem + TILE, fo16, j * KT, S, g16, mid);
+                if (!live) mid();
+                else if (jj == last_ragged) dq_tile16<D, true, NKB>(st16, smem, smem + KS * TILE, fo16, jj * KT, S, g16, mid);
+                else dq_tile16<D, false, NKB>(st16, smem, smem + KS * TILE, fo16, jj * KT, S, g16, mid);
             } else {
                 if (j == last_ragged) dq_tile<D, true, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
                 else dq_tile<D, false, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
             }
             if (more) {
-                ks.store(smem + 2 * TILE, 1.f, tid);
-                vs.store(smem + 3 * TILE, 1.f, tid);
+                ks.store(smem + 2 * KS * TILE, 1.f, tid);
+                vs.store(smem + 3 * KS * TILE, 1.f, tid);
             }
             __syncthreads();
         }
-        if (j + 1 < ntiles) {
-            const bool more = j + 2 < ntiles;
+        if (j + 1 < nsteps) {
+            const bool more = j + 2 < nsteps;
+            const int jj = (j + 1) * KS + kg;
+            const bool live = KS == 1 || jj < ntiles;
             auto ld = [&] {
-                ks.load((j + 2) * KT);
-                vs.load((j + 2) * KT);
+                ks.load((j + 2) * KS * KT);
+                vs.load((j + 2) * KS * KT);
             };
             if (more && !FA2_DQ_LP) ld();
             auto mid = [&] {
                 if (more && FA2_DQ_LP) ld();
             };
             if constexpr (M16) {
-                if (j + 1 == last_ragged)
-                    dq_tile16<D, true, NKB>(st16, smem + 2 * TILE, smem + 3 * TILE, fo16, (j + 1) * KT, S, g16, mid);
-                else dq_tile16<D, false, NKB>(st16, smem + 2 * TILE, smem + 3 * TILE, fo16, (j + 1) * KT, S, g16,
+                if (!live) mid();
+                else if (jj == last_ragged)
+                    dq_tile16<D, true, NKB>(st16, smem + 2 * KS * TILE, smem + 3 * KS * TILE, fo16, jj * KT, S, g16, mid);
+                else dq_tile16<D, false, NKB>(st16, smem + 2 * KS * TILE, smem + 3 * KS * TILE, fo16, jj * KT, S, g16,
                                               mid);
             } else {
                 if (j + 1 == last_ragged)
@@ -1061,15 +1148,41 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
             }
             if (more) {
                 ks.store(smem, 1.f, tid);
-                vs.store(smem + TILE, 1.f, tid);
+                vs.store(smem + KS * TILE, 1.f, tid);
             }
             __syncthreads();
         }
     }
 
+    if constexpr (KS > 1) {
+        // key-split merge (the loop ended on a barrier: the tile buffers are free);
+        // lane-linear records, summed in group order
+        float* mg = reinterpret_cast<float*>(smem);
+        if (kg > 0) {
+            float* rec = mg + ((kg - 1) * NQ + wave) * (D / 2) * 64;
+#pragma unroll
+            for (int md = 0; md < D / 16; ++md)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) rec[((md * 2 + nb) * 4 + i) * 64 + lane] = st16.dqa[md][nb][i];
+        }
+        __syncthreads();
+        if (kg > 0) return;  // no workgroup barrier follows
+#pragma unroll
+        for (int g = 1; g < KS; ++g) {
+            const float* rec = mg + ((g - 1) * NQ + wave) * (D / 2) * 64;
+#pragma unroll
+            for (int md = 0; md < D / 16; ++md)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) st16.dqa[md][nb][i] += rec[((md * 2 + nb) * 4 + i) * 64 + lane];
+        }
+    }
 #if FA2_BWD_COAL
     {
-        const int q0w = qb * 32 * NW + wave * 32;
+        const int q0w = qb * 32 * NQ + wave * 32;
         if constexpr (M16)
             store_block_rows16<D>(ostage[wave], st16.dqa, 1.f / __builtin_sqrtf((float)D), dQ + base + (long)q0w * D,
                                   S - q0w, lane);
@@ -1295,6 +1408,21 @@ StampLog g_dkdv_stamps;
 #endif
 // waves per workgroup: 8 x 32 keys for D <= 64 (2 waves/SIMD fit in 256 VGPRs);
 // D = 128 needs more than 256 registers per lane, so 4 waves (1 per SIMD).
+// query-split instances (QS > 1: NW / QS key waves per workgroup, 16x16x32, no stamps)
+template <int D, int NW, int QS>
+hipError_t dkdv_launch_qs(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                          const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
+#ifdef FA2_STAMPS
+    return hipErrorNotSupported;
+#else
+    const long grid = (long)bh * ((S + 32 * (NW / QS) - 1) / (32 * (NW / QS)));
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, 1, 0, true, QS>), dim3((unsigned)grid), dim3(64 * NW),
+                       0, stream, q, k, v, dout, lse, delta, dk, dv, S);
+    return hipGetLastError();
+#endif
+}
+
 template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false>
 hipError_t dkdv_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                        const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
@@ -1330,7 +1458,27 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
                          const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
     // FA2_TUNE_DKDV_WAVES = 0 (default): auto_waves over the grid of 32-key wave units
     int nw = tune_knob("DKDV_WAVES", 0);
-    if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), D <= 64 ? 8 : 4);
+    const long units = (long)bh * ((S + 31) / 32);
+    // FA2_TUNE_DKDV_QS: query groups per workgroup (0 = auto).  Auto, where 8-wave
+    // workgroups of one key block per wave would leave CUs idle: below 8 key blocks
+    // per CU QS = 2 at 8 waves; below 4, D = 32 QS = 4 at 8 waves and D = 64 QS = 2 at
+    // 4 waves (at QS = 4 its 4-tile staging registers spill).  Measured (B2_H8_D64,
+    // r01): S = 512 16.1 -> 12.1 us, 1024 29.1 -> 20.8, 2048 53.7 -> 44.3.
+    int qs = tune_knob("DKDV_QS", 0);
+    if (qs == 0 && nw == 0 && D <= 64) {
+        const int a = auto_waves(units, 8);
+        if (a == 4) qs = 2, nw = 8;
+        else if (a == 2 && D <= 32) qs = 4, nw = 8;
+        else if (a == 2) qs = 2, nw = 4;
+    }
+    if (nw == 0) nw = auto_waves(units, D <= 64 ? 8 : 4);
+    if constexpr (D <= 64) {
+        if (qs == 2 && nw == 8) return dkdv_launch_qs<D, 8, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        if (qs == 2 && nw == 4) return dkdv_launch_qs<D, 4, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+    }
+    if constexpr (D <= 32) {
+        if (qs == 4 && nw == 8) return dkdv_launch_qs<D, 8, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+    }
     const int kbk = tune_knob("DKDV_KB", 1);
 #ifdef FA2_ABLATIONS
     if constexpr (D == 64) {
@@ -1361,18 +1509,18 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     if (tune_knob("DKDV_MF4", 16) == 16) return dkdv_launch<D, 4, 1, 0, true>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
-template <int D, int NW, int NKB = 2, bool M16 = false>
+template <int D, int NW, int NKB = 2, bool M16 = false, int KS = 1>
 hipError_t dq_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                      float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
-    const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
+    const long grid = (long)bh * ((S + 32 * (NW / KS) - 1) / (32 * (NW / KS)));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
 #if FA2_BWD_COAL
     if (o)
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB, M16>), dim3((unsigned)grid),
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB, M16, KS>), dim3((unsigned)grid),
                            dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     else
 #endif
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB, M16>), dim3((unsigned)grid),
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB, M16, KS>), dim3((unsigned)grid),
                            dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     return hipGetLastError();
 }
@@ -1386,7 +1534,24 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     // seeds and the dQ accumulators alone are 160 VGPRs -- r01)
     // (D = 128 at 8 waves on 16x16x32 with 32-key tiles still spills ~70 VGPRs inside the
     // loop: Q, dO fragments and the dQ accumulators alone take 128)
-    if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), D <= 64 ? 8 : 4, D <= 64 ? 2 : 4);
+    const long units = (long)bh * ((S + 31) / 32);
+    // FA2_TUNE_DQ_KS: key groups per workgroup (0 = auto).  Auto, at 8 waves: KS = 2
+    // below 8 query blocks per CU, KS = 4 below 4 (KS = 4 runs 32-key tiles: 64-key
+    // tiles with the 4-tile staging registers spill).  Measured (B2_H8_D64 dQ + Δ,
+    // r01): S = 512 17.0 -> 11.4 us, 1024 29.5 -> 15.7, 2048 41.9 -> 36.7.
+    int ksp = tune_knob("DQ_KS", 0);
+    if (ksp == 0 && nw == 0 && D <= 64) {
+        const int a = auto_waves(units, 8);
+        if (a == 4) ksp = 2, nw = 8;
+        else if (a == 2) ksp = 4, nw = 8;
+    }
+    if (nw == 0) nw = auto_waves(units, D <= 64 ? 8 : 4, D <= 64 ? 2 : 4);
+    if constexpr (D <= 64) {
+        if (ksp == 2 && nw == 8) return dq_launch<D, 8, 2, true, 2>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        if (ksp == 4 && nw == 8) return dq_launch<D, 8, 1, true, 4>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        if (ksp == 2 && nw == 4) return dq_launch<D, 4, 2, true, 2>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+        if (ksp == 4 && nw == 4) return dq_launch<D, 4, 1, true, 4>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+    }
     // FA2_TUNE_DQ_MF: MFMA shape, 16 (16x16x32, default: +2.4 % at C3) or 32 (32x32x16)
     const bool m16 = tune_knob("DQ_MF", 16) == 16;
     if constexpr (D <= 64) {

@@ -150,6 +150,16 @@ struct FragOffsets {
             tr[b][1] = tile_off<D>(rt + 8, 32 * b + ct);
         }
     }
+    // move every offset by o halves (a wave's fixed tile inside a multi-tile image)
+    __device__ __forceinline__ void shift(int o) {
+#pragma unroll
+        for (int t = 0; t < D / 16; ++t) row[t] += o;
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b) {
+            tr[b][0] += o;
+            tr[b][1] += o;
+        }
+    }
     // A operand, k over rows r0 .. r0+15 of the tile (r0 multiple of 16), columns 32b..32b+31
     __device__ __forceinline__ f16x8 trop(const _Float16* tile, int r0, int b) const {
         return cat4(lds_tr4(tile + tr[b][0] + r0 * D), lds_tr4(tile + tr[b][1] + r0 * D));
@@ -478,7 +488,9 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
         tprev = t_;                                                                               \
     } while (0)
 #define FA2_STAMP_ARG , unsigned long long* __restrict__ stamps
+#define FA2_STAMPS_ON 1
 #else
+#define FA2_STAMPS_ON 0
 #define FA2_STAMP(k)
 #define FA2_STAMP_ARG
 #endif
@@ -559,7 +571,13 @@ __device__ __forceinline__ void fwd_loop_stag(FwdState<D> (&st)[MQ], _Float16* s
 // per wave for the scheduler to interleave, each K / V^T fragment feeding two MFMAs).
 // NKB 32-key blocks per KV tile (2: 64-key tiles; 1: 32-key tiles, fewer registers
 // for D = 128 at 8 waves).
-template <int D, int NW, int MQ, int ABL = 0, int NKB = 2>
+//
+// KS > 1 (small grids, MQ = 1): the key range is split over KS wave groups of NQ =
+// NW / KS waves.  Wave w handles query rows of slot w % NQ against tiles j·KS + w / NQ;
+// each step stages KS tiles.  The groups' (m, l, O) meet in LDS after the loop
+// (O = Σ_g 2^(m_g - m) O_g, l likewise) and group 0 stores.  That puts NW waves on
+// NQ · 32 query rows, so a grid of few query blocks still covers every SIMD twice.
+template <int D, int NW, int MQ, int ABL = 0, int NKB = 2, int KS = 1>
 __global__ void __launch_bounds__(64 * NW, (NW == 4 && D <= 64) ? FA2_FWD_W4_OCC : 1)
 fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                    float* __restrict__ O, float* __restrict__ LSE, int S FA2_STAMP_ARG) {
@@ -568,21 +586,29 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
     constexpr int QW = 32 * MQ;  // query rows per wave
-    constexpr bool STAG = FA2_FWD_STAG && NW == 8 && NKB == 2;
+    static_assert(KS == 1 || (MQ == 1 && !FA2_STAMPS_ON && NW % KS == 0), "key split: MQ = 1");
+    constexpr int NQ = NW / KS;  // query waves (KS > 1: waves w, w + NQ, ... share rows)
+    constexpr bool STAG = FA2_FWD_STAG && NW == 8 && NKB == 2 && KS == 1;
     constexpr int NSLOT = STAG ? 3 : 2;
-    // [slot][K | V] tiles; at least one Q block (coalesced prologue) in size
-    constexpr int SMEM = (2 * NSLOT * TILE > 32 * MQ * NW * D) ? 2 * NSLOT * TILE : 32 * MQ * NW * D;
+    // key-split merge records: per wave of groups 1..KS-1, O (D/2 floats per lane), m, l
+    constexpr int MREC = (D / 2 + 2) * 64;
+    constexpr int MERGE = KS > 1 ? 2 * (KS - 1) * NQ * MREC : 0;  // in halves
+    // [slot][K | V][KS] tiles; at least one Q block (coalesced prologue) and the merge
+    constexpr int SMEM0 = (2 * NSLOT * KS * TILE > 32 * MQ * NQ * D) ? 2 * NSLOT * KS * TILE : 32 * MQ * NQ * D;
+    constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;
     __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
 #if FA2_FWD_COAL
-    __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];  // per-wave O block stage
+    __shared__ __attribute__((aligned(16))) float ostage[NQ][32][36];  // per-wave O block stage
 #endif
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int nqb = (S + QW * NW - 1) / (QW * NW);
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = KS > 1 ? (tid >> 6) % NQ : tid >> 6;  // query slot of the wave
+    const int kg = KS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NQ) : 0;  // key group
+    const int nqb = (S + QW * NQ - 1) / (QW * NQ);
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = bid / nqb, qb = bid - bh * nqb;
     const long base = (long)bh * S * D;
-    const int q0 = qb * QW * NW + wave * QW + r;  // group g: query q0 + 32 g
+    const int q0 = qb * QW * NQ + wave * QW + r;  // group g: query q0 + 32 g
 
     FwdState<D> st[MQ];
     FragOffsets<D> fo;
@@ -592,9 +618,9 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     // and scaled into the (still idle) K/V LDS buffers, then read back as this wave's
     // B fragments: 1 KB per load instruction instead of 32 rows x 32 B per-lane pieces.
     {
-        TileStager<D, 32 * MQ * NW, NT> qst;
+        TileStager<D, 32 * MQ * NQ, NT> qst;
         qst.init(Q + base, S, tid);
-        qst.load(qb * QW * NW);
+        qst.load(qb * QW * NQ);
         qst.store(smem, FA2_LOG2E / __builtin_sqrtf((float)D), tid);
         __syncthreads();
 #pragma unroll
@@ -612,16 +638,21 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     // K/V staging by the first FA2_FWD_SW waves (all when 0): the second half loses
     // VALU arbitration to its SIMD partners, so the first half takes the staging
     constexpr int SW = (FA2_FWD_SW > 0 && FA2_FWD_SW < NW) ? FA2_FWD_SW : NW;
-    TileStager<D, KT, 64 * SW> ks, vs;
+    // (KS > 1: a step stages KS consecutive tiles as one [KS * KT][D] image per tensor)
+    TileStager<D, KT * KS, 64 * SW> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
-    ks.on = vs.on = __builtin_amdgcn_readfirstlane(wave) < SW;
+    ks.on = vs.on = __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
     const int ntiles = (ABL & 64) ? 1 : (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
+    const int nsteps = (ntiles + KS - 1) / KS;
+    // the group's tile within each staged image: folded into the per-lane offsets, so
+    // every LDS read keeps a compile-time tile base
+    if (KS > 1) fo.shift(kg * TILE);
     ks.load(0);
     vs.load(0);
     ks.store(smem, 1.f, tid);
-    vs.store(smem + TILE, 1.f, tid);
+    vs.store(smem + KS * TILE, 1.f, tid);
     __syncthreads();
 
     if (FA2_FWD_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
@@ -633,55 +664,63 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     unsigned long long stv[FA2_NSTAMP] = {0, 0, 0, 0, 0}, tprev;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
 #endif
-    // two tiles per trip so every LDS buffer offset is a compile-time immediate
-    for (int j = 0; j < ntiles; j += 2) {
+    // two steps per trip so every LDS buffer offset is a compile-time immediate
+    for (int j = 0; j < nsteps; j += 2) {
         {
-            const bool more = !(ABL & 1) && j + 1 < ntiles;
+            const bool more = !(ABL & 1) && j + 1 < nsteps;
+            const int jj = j * KS + kg;             // this wave's tile
+            const bool live = KS == 1 || jj < ntiles;  // wave-uniform (KS > 1: ragged tail)
             if (more && !FA2_FWD_LP) {
-                ks.load((j + 1) * KT);
-                vs.load((j + 1) * KT);
+                ks.load((j + 1) * KS * KT);
+                vs.load((j + 1) * KS * KT);
             }
             FA2_STAMP(0);
             f32x16 sacc[MQ][NKB];
-            fwd_qk<D, MQ, ABL, NKB, SEED>(sacc, st, smem, fo);
+            if (live) fwd_qk<D, MQ, ABL, NKB, SEED>(sacc, st, smem, fo);
             if (more && FA2_FWD_LP) {
-                ks.load((j + 1) * KT);
-                vs.load((j + 1) * KT);
+                ks.load((j + 1) * KS * KT);
+                vs.load((j + 1) * KS * KT);
             }
             FA2_STAMP(1);
-            if (j == last_ragged)
-                fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
-            else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sacc, smem + TILE, fo, j * KT, S, h, j == 0);
+            if (live) {
+                if (jj == last_ragged)
+                    fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sacc, smem + KS * TILE, fo, jj * KT, S, h, j == 0);
+                else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sacc, smem + KS * TILE, fo, jj * KT, S, h, j == 0);
+            }
             FA2_STAMP(2);
             if (more) {
-                ks.store(smem + 2 * TILE, 1.f, tid);
-                vs.store(smem + 3 * TILE, 1.f, tid);
+                ks.store(smem + 2 * KS * TILE, 1.f, tid);
+                vs.store(smem + 3 * KS * TILE, 1.f, tid);
             }
             FA2_STAMP(3);
             if (!(ABL & 4)) __syncthreads();
             FA2_STAMP(4);
         }
-        if (j + 1 < ntiles) {
-            const bool more = !(ABL & 1) && j + 2 < ntiles;
+        if (j + 1 < nsteps) {
+            const bool more = !(ABL & 1) && j + 2 < nsteps;
+            const int jj = (j + 1) * KS + kg;
+            const bool live = KS == 1 || jj < ntiles;
             if (more && !FA2_FWD_LP) {
-                ks.load((j + 2) * KT);
-                vs.load((j + 2) * KT);
+                ks.load((j + 2) * KS * KT);
+                vs.load((j + 2) * KS * KT);
             }
             FA2_STAMP(0);
             f32x16 sacc[MQ][NKB];
-            fwd_qk<D, MQ, ABL, NKB, SEED>(sacc, st, smem + 2 * TILE, fo);
+            if (live) fwd_qk<D, MQ, ABL, NKB, SEED>(sacc, st, smem + 2 * KS * TILE, fo);
             if (more && FA2_FWD_LP) {
-                ks.load((j + 2) * KT);
-                vs.load((j + 2) * KT);
+                ks.load((j + 2) * KS * KT);
+                vs.load((j + 2) * KS * KT);
             }
             FA2_STAMP(1);
-            if (j + 1 == last_ragged)
-                fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
-            else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sacc, smem + 3 * TILE, fo, (j + 1) * KT, S, h, false);
+            if (live) {
+                if (jj == last_ragged)
+                    fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sacc, smem + 3 * KS * TILE, fo, jj * KT, S, h, false);
+                else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sacc, smem + 3 * KS * TILE, fo, jj * KT, S, h, false);
+            }
             FA2_STAMP(2);
             if (more) {
                 ks.store(smem, 1.f, tid);
-                vs.store(smem + TILE, 1.f, tid);
+                vs.store(smem + KS * TILE, 1.f, tid);
             }
             FA2_STAMP(3);
             if (!(ABL & 4)) __syncthreads();
@@ -693,6 +732,39 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blockIdx.x * NW + wave) * FA2_NSTAMP + k] = stv[k];
 #endif
     }
+    if constexpr (KS > 1) {
+        // Key-split merge (the loop ended on a barrier: the tile buffers are free).
+        // Records are lane-linear ([value][lane]), so writes and reads are conflict-free;
+        // a group that got no tile (kg >= ntiles) reports m = -inf, weight 0.
+        float* mg = reinterpret_cast<float*>(smem);
+        if (kg > 0) {
+            float* rec = mg + ((kg - 1) * NQ + wave) * MREC;
+#pragma unroll
+            for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) rec[(16 * b + i) * 64 + lane] = st[0].oacc[b][i];
+            rec[(D / 2) * 64 + lane] = kg < ntiles ? st[0].m : -__builtin_inff();
+            rec[(D / 2 + 1) * 64 + lane] = (st[0].l[0] + st[0].l[1]) + (st[0].l[2] + st[0].l[3]);
+        }
+        __syncthreads();
+        if (kg > 0) return;  // no workgroup barrier follows
+        float l = (st[0].l[0] + st[0].l[1]) + (st[0].l[2] + st[0].l[3]);
+#pragma unroll
+        for (int g = 1; g < KS; ++g) {
+            const float* rec = mg + ((g - 1) * NQ + wave) * MREC;
+            const float mo = rec[(D / 2) * 64 + lane];
+            const float mx = fmaxf(st[0].m, mo);
+            const float a = fast_exp2(st[0].m - mx), ao = fast_exp2(mo - mx);
+#pragma unroll
+            for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) st[0].oacc[b][i] = st[0].oacc[b][i] * a + rec[(16 * b + i) * 64 + lane] * ao;
+            l = l * a + rec[(D / 2 + 1) * 64 + lane] * ao;
+            st[0].m = mx;
+        }
+        st[0].l[0] = l;
+        st[0].l[1] = st[0].l[2] = st[0].l[3] = 0.f;
+    }
 #if FA2_FWD_COAL
     // O through a wave-private LDS stage, one 32x32 block at a time, stored as whole
     // 128-B row segments (8 rows per instruction) instead of 16-B pieces of 32 rows
@@ -700,7 +772,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     for (int g = 0; g < MQ; ++g) {
         const float lt = xor32_sum((st[g].l[0] + st[g].l[1]) + (st[g].l[2] + st[g].l[3]));
         const float inv = 1.f / lt;
-        const int qrow0 = qb * QW * NW + wave * QW + 32 * g;  // first row of this group
+        const int qrow0 = qb * QW * NQ + wave * QW + 32 * g;  // first row of this group
         float(*os)[36] = ostage[wave];
 #pragma unroll
         for (int b = 0; b < D / 32; ++b) {
@@ -1096,6 +1168,23 @@ static void fwd_f16_go(const float* q, const float* k, const float* v, float* o,
 #endif
 }
 
+// key-split instances (KS > 1: NW / KS query waves per workgroup, no stamps/ablations)
+// (D = 64: 32-key tiles -- with 64-key tiles the KS-tile staging registers spill)
+template <int D, int NW, int KS, int NKB = (D <= 32 ? 2 : 1)>
+static hipError_t fwd_f16_launch_ks(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
+                                    hipStream_t stream) {
+#ifdef FA2_STAMPS
+    return hipErrorNotSupported;
+#else
+    const int nqb = (S + 32 * (NW / KS) - 1) / (32 * (NW / KS));
+    const long grid = (long)bh * nqb;
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, 1, 0, NKB, KS>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q,
+                       k, v, o, lse, S);
+    return hipGetLastError();
+#endif
+}
+
 template <int D, int NW, int MQ = 1, int NKB = 2>
 static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
                                  hipStream_t stream) {
@@ -1134,8 +1223,26 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     // (MQ = 2, two 32-row query groups per wave at 4 waves / 1 per SIMD, measured
     // 30 % slower than 8 waves x 1 group at D = 32 and 64 -- r01)
     // FA2_TUNE_FWD_WAVES = 0 (default): auto_waves over the grid of 32-query wave units
+    const long units = (long)bh * ((S + 31) / 32);
     int nw = tune_knob("FWD_WAVES", 0);
-    if (nw == 0) nw = auto_waves((long)bh * ((S + 31) / 32), 8);
+    // FA2_TUNE_FWD_KS: key groups per workgroup (0 = auto).  Auto: where even 4-wave
+    // workgroups would leave CUs idle (< 4 query blocks per CU), split the key range
+    // 4 ways instead of shrinking the workgroup -- 8 waves on 64 query rows, or 4 waves
+    // on 32 rows below 2 query blocks per CU.  Measured (B2_H8_D64 fwd, r01):
+    // S = 512 12.4 -> 9.9 us, S = 1024 21.4 -> 15.4 us; at S = 2048 (4 blocks per CU)
+    // KS = 2 on 32-key tiles ties the unsplit 4-wave kernel (35.9 vs 34.8 us).
+    int ks = tune_knob("FWD_KS", 0);
+    if (ks == 0 && nw == 0 && D <= 64 && auto_waves(units, 8) == 2) {
+        ks = 4;
+        nw = auto_waves(units, 2, 1) == 2 ? 8 : 4;
+    }
+    if (nw == 0) nw = auto_waves(units, 8);
+    if constexpr (D <= 64) {
+        if (ks == 2 && nw == 8) return fwd_f16_launch_ks<D, 8, 2>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 4 && nw == 8) return fwd_f16_launch_ks<D, 8, 4>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 4 && nw == 4) return fwd_f16_launch_ks<D, 4, 4>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 2 && nw == 4) return fwd_f16_launch_ks<D, 4, 2>(q, k, v, o, lse, bh, S, stream);
+    }
     // FA2_TUNE_FWD_MF: MFMA shape, 32 (32x32x16) or 16 (16x16x32, fa2_fwd16_kernel)
     if (tune_knob("FWD_MF", 32) == 16) {
         constexpr int NKB16 = D <= 64 ? 2 : 1;
