@@ -530,6 +530,103 @@ __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* 
     }
 }
 
+// FA2_DKDV_PIPE: the two 32-query blocks of a step software-pipelined inside the
+// wave (one basic block after mid()): S/dP MFMAs of block 1 are issued beside the
+// exp / dS VALU of block 0, and the dV/dK MFMAs of block 0 beside the VALU of block 1,
+// so each wave overlaps its own matrix and vector work instead of relying on its
+// SIMD partner only.  1 = source order only, 2 = plus sched_group_barrier interleave.
+#ifndef FA2_DKDV_PIPE
+#define FA2_DKDV_PIPE 0
+#endif
+
+template <int D>
+struct Dkdv16Blk {
+    f32x4 sa[2][2], da[2][2];  // [mb][nb]
+};
+
+template <int D>
+__device__ __forceinline__ void dkdv16_sdp(Dkdv16Blk<D>& b, const DkdvState16<D>& st, const _Float16* Qs,
+                                           const _Float16* dOs, const float* nlse2, const float* ndel,
+                                           const FragOffsets16<D>& fo, int g, int qb) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(nlse2 + qb * 32 + 16 * mb + 4 * g);
+        const f32x4 dv = *reinterpret_cast<const f32x4*>(ndel + qb * 32 + 16 * mb + 4 * g);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            b.sa[mb][nb] = lv;
+            b.da[mb][nb] = dv;
+        }
+    }
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const f16x8 qa = fo.rowop(Qs, qb * 32 + 16 * mb, ks), doa = fo.rowop(dOs, qb * 32 + 16 * mb, ks);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                b.sa[mb][nb] = mfma16(qa, st.kf[nb][ks], b.sa[mb][nb]);
+                b.da[mb][nb] = mfma16(doa, st.vf[nb][ks], b.da[mb][nb]);
+            }
+        }
+}
+
+template <int D>
+__device__ __forceinline__ void dkdv16_soft(const Dkdv16Blk<D>& b, f16x8 (&pf)[2], f16x8 (&dsf)[2]) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float pv = fast_exp2(b.sa[j >> 2][nb][j & 3]);
+            pf[nb][j] = to_tile(pv);
+            dsf[nb][j] = to_tile(pv * b.da[j >> 2][nb][j & 3]);
+        }
+}
+
+template <int D>
+__device__ __forceinline__ void dkdv16_acc(DkdvState16<D>& st, const f16x8 (&pf)[2], const f16x8 (&dsf)[2],
+                                           const _Float16* Qs, const _Float16* dOs, const FragOffsets16<D>& fo,
+                                           int qb) {
+#pragma unroll
+    for (int md = 0; md < D / 16; ++md) {
+        const f16x8 a_do = fo.trop(dOs, qb * 32, md), a_q = fo.trop(Qs, qb * 32, md);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            st.dva[md][nb] = mfma16(a_do, pf[nb], st.dva[md][nb]);
+            st.dka[md][nb] = mfma16(a_q, dsf[nb], st.dka[md][nb]);
+        }
+    }
+}
+
+// interleave the last `nm` MFMAs with `nv` VALU each (sched_group_barrier masks:
+// 0x8 MFMA, 0x2 VALU, 0x100 DS read)
+template <int NM, int NV>
+__device__ __forceinline__ void interleave_mfma_valu() {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+    }
+}
+
+template <int D, typename Mid>
+__device__ __forceinline__ void dkdv_step16_pipe(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
+                                                 const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
+                                                 int g, Mid&& mid) {
+    Dkdv16Blk<D> b0, b1;
+    f16x8 pf0[2], dsf0[2], pf1[2], dsf1[2];
+    dkdv16_sdp<D>(b0, st, Qs, dOs, nlse2, ndel, fo, g, 0);
+    mid();
+    dkdv16_sdp<D>(b1, st, Qs, dOs, nlse2, ndel, fo, g, 1);
+    dkdv16_soft<D>(b0, pf0, dsf0);
+    if (FA2_DKDV_PIPE == 2) interleave_mfma_valu<D / 4, 3>();
+    dkdv16_acc<D>(st, pf0, dsf0, Qs, dOs, fo, 0);
+    dkdv16_soft<D>(b1, pf1, dsf1);
+    if (FA2_DKDV_PIPE == 2) interleave_mfma_valu<D / 4, 3>();
+    dkdv16_acc<D>(st, pf1, dsf1, Qs, dOs, fo, 1);
+}
+
 // a wave's 32 keys x D results (16x16 accumulator layout) through its LDS stage,
 // stored as whole 128-B row segments
 template <int D>
@@ -751,8 +848,10 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
                 if (more) load_b(it + 1);
             };
             if constexpr (M16) {
-                if (live) dkdv_step16<D, ABL>(st16, smem, smem + QS * TILE, rows[0][0] + rq, rows[0][1] + rq, fo16, g16, mid);
-                else mid();
+                if (!live) mid();
+                else if (FA2_DKDV_PIPE && ABL == 0)
+                    dkdv_step16_pipe<D>(st16, smem, smem + QS * TILE, rows[0][0] + rq, rows[0][1] + rq, fo16, g16, mid);
+                else dkdv_step16<D, ABL>(st16, smem, smem + QS * TILE, rows[0][0] + rq, rows[0][1] + rq, fo16, g16, mid);
             } else
                 dkdv_step<D, KB, ABL>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h, mid);
             FA2_STAMP(1);
@@ -770,10 +869,12 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
                 if (more) load_b(it + 2);
             };
             if constexpr (M16) {
-                if (live)
-                    dkdv_step16<D, ABL>(st16, smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0] + rq, rows[1][1] + rq,
-                                        fo16, g16, mid);
-                else mid();
+                if (!live) mid();
+                else if (FA2_DKDV_PIPE && ABL == 0)
+                    dkdv_step16_pipe<D>(st16, smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0] + rq,
+                                        rows[1][1] + rq, fo16, g16, mid);
+                else dkdv_step16<D, ABL>(st16, smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0] + rq,
+                                         rows[1][1] + rq, fo16, g16, mid);
             } else
                 dkdv_step<D, KB, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h, mid);
             FA2_STAMP(1);
