@@ -406,10 +406,12 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
         tprev = t_;                                                                               \
     } while (0)
 #define FA2_STAMP_ARG , unsigned long long* __restrict__ stamps
+#define FA2_STAMP_PASS , stamps
 #define FA2_STAMPS_ON 1
 #else
 #define FA2_STAMP(k)
 #define FA2_STAMP_ARG
+#define FA2_STAMP_PASS
 #define FA2_STAMPS_ON 0
 #endif
 
@@ -659,33 +661,46 @@ __device__ __forceinline__ void store_block_rows16(float (*os)[36], const f32x4 
 // of NK = NW / QS waves.  Wave w keeps keys of slot w % NK and takes query tiles
 // it·QS + w / NK; each step stages QS tiles.  After the loop the groups' dKᵀ / dVᵀ
 // are summed in LDS in group order (deterministic) and group 0 stores.
+// The workgroup's LDS: [buf][Q | dO][QS] fp16 tiles (or the query-split merge
+// records), [buf][-lse2 | -delta][QS] fp32 rows, the per-wave result stage.  Carved
+// from one block so the fused backward kernel can overlay it with the dQ role's.
+template <int D, int NW, int QS>
+struct DkdvLds {
+    static constexpr int QT = 64, TILE = QT * D, NK = NW / QS;
+    // query-split merge records: per wave of groups 1..QS-1, dKᵀ and dVᵀ (D floats per lane)
+    static constexpr int MERGE = QS > 1 ? 2 * (QS - 1) * NK * D * 64 : 0;  // in halves
+    static constexpr int SMEM = 2 * 2 * QS * TILE > MERGE ? 2 * 2 * QS * TILE : MERGE;  // halves
+    static constexpr int ROWS = 2 * SMEM;                      // byte offsets
+    static constexpr int OSTAGE = ROWS + 2 * 2 * QS * QT * 4;
+    static constexpr int BYTES = OSTAGE + (FA2_BWD_COAL ? NK * 32 * 36 * 4 : 0);
+};
+
+// One workgroup of the dK/dV kernel; `bid` is its (XCD-remapped) block number over
+// the BH * ceil(S / (KPW * NK)) key blocks, `blk` the raw one (stamp records only).
 template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false, int QS = 1>
-__global__ void __launch_bounds__(64 * NW)
-fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                        const float* __restrict__ dO, const float* __restrict__ LSE,
-                        const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV,
-                        int S FA2_STAMP_ARG) {
-    constexpr int QT = 64;  // query rows per step
+__device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int blk, const float* __restrict__ Q,
+                                          const float* __restrict__ K, const float* __restrict__ V,
+                                          const float* __restrict__ dO, const float* __restrict__ LSE,
+                                          const float* __restrict__ Delta, float* __restrict__ dK,
+                                          float* __restrict__ dV, int S FA2_STAMP_ARG) {
+    using L = DkdvLds<D, NW, QS>;
+    constexpr int QT = L::QT;  // query rows per step
     constexpr int NT = 64 * NW;
-    constexpr int TILE = QT * D;
+    constexpr int TILE = L::TILE;
     constexpr int KPW = 32 * KB;  // keys per wave
     static_assert(QS == 1 || (M16 && 2 * QS <= NW && !FA2_STAMPS_ON), "query split: 16x16x32, 2 QS row waves");
-    constexpr int NK = NW / QS;  // key waves (QS > 1: waves w, w + NK, ... share keys)
-    // query-split merge records: per wave of groups 1..QS-1, dKᵀ and dVᵀ (D floats per lane)
-    constexpr int MERGE = QS > 1 ? 2 * (QS - 1) * NK * D * 64 : 0;  // in halves
-    constexpr int SMEM = 2 * 2 * QS * TILE > MERGE ? 2 * 2 * QS * TILE : MERGE;
-    // [buf][Q | dO][QS] fp16 tiles, then [buf][-lse2 | -delta][QS] fp32 rows
-    __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
-    __shared__ __attribute__((aligned(16))) float rows[2][2][QS * QT];
+    constexpr int NK = L::NK;  // key waves (QS > 1: waves w, w + NK, ... share keys)
+    _Float16* smem = reinterpret_cast<_Float16*>(lds);
+    float(*rows)[2][QS * QT] = reinterpret_cast<float(*)[2][QS * QT]>(lds + L::ROWS);
 #if FA2_BWD_COAL
-    __shared__ __attribute__((aligned(16))) float ostage[NK][32][36];  // per-wave result stage
+    float(*ostage)[32][36] = reinterpret_cast<float(*)[32][36]>(lds + L::OSTAGE);  // per-wave result stage
 #endif
+    (void)blk;
 
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = QS > 1 ? (tid >> 6) % NK : tid >> 6;  // key slot of the wave
     const int qg = QS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NK) : 0;  // query group
     const int nkb = (S + KPW * NK - 1) / (KPW * NK);
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = bid / nkb, kblk = bid - bh * nkb;
     const long base = (long)bh * S * D;
     const long rbase = (long)bh * S;
@@ -886,7 +901,7 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     }
 #ifdef FA2_STAMPS
     if (lane == 0)
-        for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blockIdx.x * NW + wave) * FA2_NSTAMP + k] = stv[k];
+        for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blk * NW + wave) * FA2_NSTAMP + k] = stv[k];
 #endif
 
     if constexpr (QS > 1) {
@@ -955,6 +970,17 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
         }
     }
 #endif
+}
+
+template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false, int QS = 1>
+__global__ void __launch_bounds__(64 * NW)
+fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                        const float* __restrict__ dO, const float* __restrict__ LSE,
+                        const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV,
+                        int S FA2_STAMP_ARG) {
+    __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, QS>::BYTES];
+    dkdv_body<D, NW, KB, ABL, M16, QS>(lds, xcd_remap(blockIdx.x, gridDim.x), blockIdx.x, Q, K, V, dO, LSE, Delta, dK,
+                                       dV, S FA2_STAMP_PASS);
 }
 
 // ---------------------------------------------------------------------------
@@ -1071,31 +1097,44 @@ __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, 
 // NQ = NW / KS waves.  Wave w keeps query rows of slot w % NQ and takes K/V tiles
 // j·KS + w / NQ; each step stages KS tiles.  After the loop the groups' dQᵀ are
 // summed in LDS in group order (deterministic) and group 0 stores.
-template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1>
-__global__ void __launch_bounds__(64 * NW)
-fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                      const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
-                      float* __restrict__ dQ, int S, const float* __restrict__ O) {
-    constexpr int KT = 32 * NKB;
-    constexpr int NT = 64 * NW;
-    constexpr int TILE = KT * D;
-    static_assert(KS == 1 || (M16 && NW % KS == 0), "key split: 16x16x32");
-    constexpr int NQ = NW / KS;  // query waves (KS > 1: waves w, w + NQ, ... share rows)
+// The workgroup's LDS: [buf][K | V][KS] tiles (at least one Q block for the coalesced
+// prologue, and the key-split merge records), the per-wave dQ stage, the block's Δ.
+template <int D, int NW, bool DELTA, int NKB, int KS>
+struct DqLds {
+    static constexpr int KT = 32 * NKB, TILE = KT * D, NQ = NW / KS;
     // key-split merge records: per wave of groups 1..KS-1, dQᵀ (D / 2 floats per lane)
-    constexpr int MERGE = KS > 1 ? 2 * (KS - 1) * NQ * (D / 2) * 64 : 0;  // in halves
-    // [buf][K | V][KS] tiles; at least one Q block (coalesced prologue) and the merge
-    constexpr int SMEM0 = (4 * KS * TILE > 32 * NQ * D) ? 4 * KS * TILE : 32 * NQ * D;
-    constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;
-    __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
+    static constexpr int MERGE = KS > 1 ? 2 * (KS - 1) * NQ * (D / 2) * 64 : 0;  // in halves
+    static constexpr int SMEM0 = (4 * KS * TILE > 32 * NQ * D) ? 4 * KS * TILE : 32 * NQ * D;
+    static constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;  // halves
+    static constexpr int OSTAGE = 2 * SMEM;                     // byte offsets
+    static constexpr int DBLK = OSTAGE + (FA2_BWD_COAL ? NQ * 32 * 36 * 4 : 0);
+    static constexpr int BYTES = DBLK + (DELTA ? 32 * NQ : 1) * 4;
+};
+
+// One workgroup of the dQ kernel; `bid` is its (XCD-remapped) block number over the
+// BH * ceil(S / (32 * NQ)) query blocks.
+template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1>
+__device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const float* __restrict__ Q,
+                                        const float* __restrict__ K, const float* __restrict__ V,
+                                        const float* __restrict__ dO, const float* __restrict__ LSE,
+                                        float* __restrict__ Delta, float* __restrict__ dQ, int S,
+                                        const float* __restrict__ O) {
+    using L = DqLds<D, NW, DELTA, NKB, KS>;
+    constexpr int KT = L::KT;
+    constexpr int NT = 64 * NW;
+    constexpr int TILE = L::TILE;
+    static_assert(KS == 1 || (M16 && NW % KS == 0), "key split: 16x16x32");
+    constexpr int NQ = L::NQ;  // query waves (KS > 1: waves w, w + NQ, ... share rows)
+    _Float16* smem = reinterpret_cast<_Float16*>(lds);
 #if FA2_BWD_COAL
-    __shared__ __attribute__((aligned(16))) float ostage[NQ][32][36];  // per-wave dQ stage
+    float(*ostage)[32][36] = reinterpret_cast<float(*)[32][36]>(lds + L::OSTAGE);  // per-wave dQ stage
 #endif
+    float* delta_blk = reinterpret_cast<float*>(lds + L::DBLK);
 
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = KS > 1 ? (tid >> 6) % NQ : tid >> 6;  // query slot of the wave
     const int kg = KS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NQ) : 0;  // key group
     const int nqb = (S + 32 * NQ - 1) / (32 * NQ);
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = bid / nqb, qb = bid - bh * nqb;
     const long base = (long)bh * S * D;
     const int q = qb * 32 * NQ + wave * 32 + r;
@@ -1123,7 +1162,6 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
         for (int t = 0; t < D / 16; ++t) st.qf[t] = fo.rowop(smem, wave * 32, t);
     }
     __syncthreads();
-    __shared__ float delta_blk[DELTA ? 32 * NQ : 1];
     if (DELTA)
         stage_block_delta<D, 32 * NQ, NT>(smem, dO + base, O + base, S, qb * 32 * NQ, delta_blk,
                                           Delta + (long)bh * S, tid);
@@ -1306,6 +1344,39 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     }
 #endif
 }
+
+template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1>
+__global__ void __launch_bounds__(64 * NW)
+fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                      const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
+                      float* __restrict__ dQ, int S, const float* __restrict__ O) {
+    __shared__ __attribute__((aligned(16))) char lds[DqLds<D, NW, DELTA, NKB, KS>::BYTES];
+    dq_body<D, NW, DELTA, NKB, M16, KS>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE, Delta, dQ, S, O);
+}
+
+#ifndef FA2_STAMPS
+// dK/dV and dQ in ONE launch (small grids).  Workgroups [0, ndk) take the dK/dV role
+// (QS query groups), [ndk, gridDim.x) the dQ role (KS key groups); the two roles
+// share nothing, so they run side by side on the chip instead of one kernel after
+// the other, and the second launch's ramp-up and tail go away.  Δ comes from a
+// prior fa2_delta_kernel (the dQ role cannot hand its fused Δ to the dK/dV role
+// without a cross-workgroup wait).  Both roles run 8 waves on the 16x16x32 path;
+// the LDS block is the larger of the two layouts, registers the larger of the two.
+template <int D, int QS, int KS, int NKB>
+__global__ void __launch_bounds__(512)
+fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                         const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+                         float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV, int S, int ndk) {
+    constexpr int B1 = DkdvLds<D, 8, QS>::BYTES, B2 = DqLds<D, 8, false, NKB, KS>::BYTES;
+    __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
+    const int b = blockIdx.x;
+    if (b < ndk)
+        dkdv_body<D, 8, 1, 0, true, QS>(lds, xcd_remap(b, ndk), b, Q, K, V, dO, LSE, Delta, dK, dV, S);
+    else
+        dq_body<D, 8, false, NKB, true, KS>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
+                                            const_cast<float*>(Delta), dQ, S, nullptr);
+}
+#endif
 
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
 // block 256, test_flash_attention2.py:499-535 / f-attn2-backward_f16.cu:445),
@@ -1703,10 +1774,70 @@ hipError_t FA2_TILE_LAUNCH(launch_bwd_dq_delta)(int D, const float* q, const flo
     }
 }
 
-// Δ fused into the dQ kernel's prologue (which stages dO anyway); dK/dV reads it.
+namespace {
+#ifndef FA2_STAMPS
+template <int D, int QS, int KS, int NKB>
+hipError_t fused_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                        const float* delta, float* dq, float* dk, float* dv, int bh, int S, hipStream_t stream) {
+    const long ndk = (long)bh * ((S + 32 * (8 / QS) - 1) / (32 * (8 / QS)));
+    const long ndq = (long)bh * ((S + 32 * (8 / KS) - 1) / (32 * (8 / KS)));
+    if (ndk <= 0 || ndq <= 0 || ndk + ndq > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_fused_f16_kernel<D, QS, KS, NKB>), dim3((unsigned)(ndk + ndq)), dim3(512), 0,
+                       stream, q, k, v, dout, lse, delta, dq, dk, dv, S, (int)ndk);
+    return hipGetLastError();
+}
+#endif
+// The fused dK/dV + dQ launch for D <= 64, or hipErrorNotSupported (then the caller
+// runs the two kernels).  Split factors follow the separate kernels' auto rule:
+// below 4 blocks of 32 rows per CU QS = 2 / KS = 4 (32-key tiles), below 8 QS = 2 /
+// KS = 2, else unsplit.  FA2_TUNE_BWD_FQS / FA2_TUNE_BWD_FKS force them.
+template <int D>
+hipError_t fused_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                          const float* delta, float* dq, float* dk, float* dv, int bh, int S, hipStream_t stream) {
+#ifdef FA2_STAMPS
+    return hipErrorNotSupported;
+#else
+    if constexpr (D > 64) {
+        return hipErrorNotSupported;
+    } else {
+        const int a = auto_waves((long)bh * ((S + 31) / 32), 8);
+        const int fqs = tune_knob("BWD_FQS", a == 8 ? 1 : 2), fks = tune_knob("BWD_FKS", a == 8 ? 1 : a == 4 ? 2 : 4);
+        if (fqs == 1 && fks == 1) return fused_launch<D, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        if (fqs == 2 && fks == 2) return fused_launch<D, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        if (fqs == 2 && fks == 4) return fused_launch<D, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        return hipErrorNotSupported;
+    }
+#endif
+}
+}  // namespace
+
+hipError_t FA2_TILE_LAUNCH(launch_bwd_fused)(int D, const float* q, const float* k, const float* v, const float* dout,
+                                const float* lse, const float* delta, float* dq, float* dk, float* dv, int bh, int S,
+                                hipStream_t stream) {
+    if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
+    switch (D) {
+        case 32: return fused_dispatch<32>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        case 64: return fused_dispatch<64>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        default: return hipErrorNotSupported;
+    }
+}
+
+// FA2_TUNE_BWD_FUSED: 1 = Δ kernel, then dK/dV and dQ in one launch (D <= 64);
+// 0 = Δ fused into the dQ kernel's prologue (which stages dO anyway), then dK/dV,
+// which reads it; -1 (default) = 1 on grids of fewer than 8 blocks of 32 rows per
+// CU.  Measured (fwd + bwd step, B2_H8_D64, r01): S = 512 31.1 -> 27.0 us, 1024
+// 50.1 -> 48.2, 2048 108.7 -> 106.0; S = 4096 282 -> 286 and C3 +-0 (so unfused).
 hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream) {
+    int fused = tune_knob("BWD_FUSED", -1);
+    if (fused < 0) fused = bh > 0 && S > 0 && auto_waves((long)bh * ((S + 31) / 32), 8) < 8;
+    if (D <= 64 && bh > 0 && S > 0 && fused == 1) {
+        hipError_t e = launch_delta(D, dout, o, delta, bh, S, stream);
+        if (e != hipSuccess) return e;
+        e = FA2_TILE_LAUNCH(launch_bwd_fused)(D, q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        if (e != hipErrorNotSupported) return e;
+    }
     hipError_t e = FA2_TILE_LAUNCH(launch_bwd_dq_delta)(D, q, k, v, o, dout, lse, delta, dq, bh, S, stream);
     if (e != hipSuccess) return e;
     return FA2_TILE_LAUNCH(launch_bwd_dkdv)(D, q, k, v, dout, lse, delta, dk, dv, bh, S, stream);

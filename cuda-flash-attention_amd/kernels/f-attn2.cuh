@@ -95,6 +95,12 @@ hipError_t launch_bwd_dq_delta_f16(int D, const float* q, const float* k, const 
                                    const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
                                    hipStream_t stream);
 
+// Δ given: dK/dV and dQ as ONE launch (two workgroup roles side by side; D <= 64,
+// else hipErrorNotSupported)
+hipError_t launch_bwd_fused_f16(int D, const float* q, const float* k, const float* v, const float* dout,
+                                const float* lse, const float* delta, float* dq, float* dk, float* dv, int bh, int S,
+                                hipStream_t stream);
+
 // bf16-tile twins of the *_f16 launchers above (kernels built from the same source)
 hipError_t launch_forward_bf16(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,
                                int S, hipStream_t stream);
@@ -106,6 +112,9 @@ hipError_t launch_bwd_dkdv_bf16(int D, const float* q, const float* k, const flo
                                 hipStream_t stream);
 hipError_t launch_bwd_dq_bf16(int D, const float* q, const float* k, const float* v, const float* dout,
                               const float* lse, const float* delta, float* dq, int bh, int S, hipStream_t stream);
+hipError_t launch_bwd_fused_bf16(int D, const float* q, const float* k, const float* v, const float* dout,
+                                 const float* lse, const float* delta, float* dq, float* dk, float* dv, int bh, int S,
+                                 hipStream_t stream);
 hipError_t launch_bwd_dq_delta_bf16(int D, const float* q, const float* k, const float* v, const float* o,
                                     const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
                                     hipStream_t stream);

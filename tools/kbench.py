@@ -36,7 +36,7 @@ def main():
     o, lse = fa2amd.forward(q, k, v, "fp16")
     dl = fa2amd.delta(do, o)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
-    flops = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "dqd": 2.0, "delta": 0.0, "bwd": 10.0, "step": 14.0,
+    flops = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "dqd": 2.0, "delta": 0.0, "bwd": 10.0, "step": 14.0, "stepb": 14.0,
              "step3": 14.0, "step2s": 14.0, "step2r": 14.0}
     s2 = torch.cuda.Stream(device=dev)
 
@@ -68,6 +68,9 @@ def main():
                          fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
                          fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv)),
         "dqd": lambda: fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
+        # fwd + fa2_backward (whatever launch plan launch_backward picks, e.g. FA2_TUNE_BWD_FUSED)
+        "stepb": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
+                          fa2amd.backward(q, k, v, o, do, lse, "fp16", dq=dq, dk=dk, dv=dv, delta_buf=dl)),
         # dK/dV and dQ on two streams after a separate delta kernel
         "step2s": lambda: two_stream_step(True),
         "step2r": lambda: two_stream_step(False),
