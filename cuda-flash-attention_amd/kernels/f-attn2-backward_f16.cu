@@ -237,16 +237,9 @@ __device__ __forceinline__ void stage_block(_Float16* lds, const float* head_bas
 // row's chunks are consecutive lanes, reduced with xor shuffles.  Δ goes to
 // `delta_lds` (this workgroup's rows) and to HBM for the dK/dV kernel.
 template <int D, int ROWS, int NT>
-__device__ __forceinline__ void stage_block_delta(_Float16* lds, const float* dO_head, const float* O_head, int S,
-                                                  int row0, float* delta_lds, float* __restrict__ delta_out,
-                                                  int tid) {
+__device__ __forceinline__ void delta_rows(const TileStager<D, ROWS, NT>& a, const TileStager<D, ROWS, NT>& o, int S,
+                                           int row0, float* delta_lds, float* __restrict__ delta_out, int tid) {
     using TS = TileStager<D, ROWS, NT>;
-    TS a, o;
-    a.init(dO_head, S, tid);
-    o.init(O_head, S, tid);
-    a.load(row0);
-    o.load(row0);
-    a.store(lds, 1.f, tid);
 #pragma unroll
     for (int c = 0; c < TS::CPT; ++c) {
         const int x = tid + c * NT;
@@ -260,6 +253,18 @@ __device__ __forceinline__ void stage_block_delta(_Float16* lds, const float* dO
             if (row0 + row < S) delta_out[row0 + row] = d;
         }
     }
+}
+template <int D, int ROWS, int NT>
+__device__ __forceinline__ void stage_block_delta(_Float16* lds, const float* dO_head, const float* O_head, int S,
+                                                  int row0, float* delta_lds, float* __restrict__ delta_out,
+                                                  int tid) {
+    TileStager<D, ROWS, NT> a, o;
+    a.init(dO_head, S, tid);
+    o.init(O_head, S, tid);
+    a.load(row0);
+    o.load(row0);
+    a.store(lds, 1.f, tid);
+    delta_rows<D, ROWS, NT>(a, o, S, row0, delta_lds, delta_out, tid);
 }
 
 // a wave's 32 x D accumulator block (row d = 32b + (i&3) + 8(i>>2) + 4h of the
@@ -664,12 +669,18 @@ __device__ __forceinline__ void store_block_rows16(float (*os)[36], const f32x4 
 // The workgroup's LDS: [buf][Q | dO][QS] fp16 tiles (or the query-split merge
 // records), [buf][-lse2 | -delta][QS] fp32 rows, the per-wave result stage.  Carved
 // from one block so the fused backward kernel can overlay it with the dQ role's.
-template <int D, int NW, int QS>
+template <int D, int NW, int KB, int QS>
 struct DkdvLds {
     static constexpr int QT = 64, TILE = QT * D, NK = NW / QS;
     // query-split merge records: per wave of groups 1..QS-1, dKᵀ and dVᵀ (D floats per lane)
     static constexpr int MERGE = QS > 1 ? 2 * (QS - 1) * NK * D * 64 : 0;  // in halves
-    static constexpr int SMEM = 2 * 2 * QS * TILE > MERGE ? 2 * 2 * QS * TILE : MERGE;  // halves
+    // OVL: the prologue's K and V blocks side by side, loaded together with the first
+    // Q/dO step (small grids, where the prologue's round trips are exposed; on the
+    // unsplit C3 grid it measured -1.2 %)
+    static constexpr bool OVL = QS > 1;
+    static constexpr int KV = OVL ? 2 * 32 * KB * NK * D : 0;
+    static constexpr int SMEM0 = 2 * 2 * QS * TILE > MERGE ? 2 * 2 * QS * TILE : MERGE;
+    static constexpr int SMEM = (FA2_BWD_COAL && KV > SMEM0) ? KV : SMEM0;  // halves
     static constexpr int ROWS = 2 * SMEM;                      // byte offsets
     static constexpr int OSTAGE = ROWS + 2 * 2 * QS * QT * 4;
     static constexpr int BYTES = OSTAGE + (FA2_BWD_COAL ? NK * 32 * 36 * 4 : 0);
@@ -683,7 +694,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
                                           const float* __restrict__ dO, const float* __restrict__ LSE,
                                           const float* __restrict__ Delta, float* __restrict__ dK,
                                           float* __restrict__ dV, int S FA2_STAMP_ARG) {
-    using L = DkdvLds<D, NW, QS>;
+    using L = DkdvLds<D, NW, KB, QS>;
     constexpr int QT = L::QT;  // query rows per step
     constexpr int NT = 64 * NW;
     constexpr int TILE = L::TILE;
@@ -718,29 +729,57 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
     if constexpr (M16) fo16.init(lane);
     (void)r;
 #if FA2_BWD_COAL
+    // Prologue.  L::OVL: the K and V blocks and the first Q/dO step are loaded in one
+    // go (one HBM round trip instead of three), K and V side by side in the LDS block;
+    // else K, then V, each through the Q/dO buffers.
     static_assert(KPW * NK <= 4 * QT, "K / V block fits the Q/dO buffers");
     const int kblock0 = kblk * KPW * NK;
-    stage_block<D, KPW * NK, NT>(smem, K + base, S, kblock0, kscale, tid);
-    __syncthreads();
-    if constexpr (M16) {
+    _Float16* const vblk = L::OVL ? smem + KPW * NK * D : smem;
+    auto read_k = [&] {
+        if constexpr (M16) {
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+            for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-            for (int ks = 0; ks < D / 32; ++ks) st16.kf[nb][ks] = fo16.rowop(smem, wave * KPW + 16 * nb, ks);
-    } else {
+                for (int ks = 0; ks < D / 32; ++ks) st16.kf[nb][ks] = fo16.rowop(smem, wave * KPW + 16 * nb, ks);
+        } else {
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
+            for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-            for (int t = 0; t < D / 16; ++t) st.kf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
+                for (int t = 0; t < D / 16; ++t) st.kf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
+        }
+    };
+    auto read_v = [&] {
+        if constexpr (M16) {
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int ks = 0; ks < D / 32; ++ks) st16.vf[nb][ks] = fo16.rowop(vblk, wave * KPW + 16 * nb, ks);
+        } else {
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+                for (int t = 0; t < D / 16; ++t) st.vf[kb][t] = fo.rowop(vblk, wave * KPW + kb * 32, t);
+        }
+    };
+    TileStager<D, KPW * NK, NT> kst, vst;
+    kst.init(K + base, S, tid);
+    vst.init(V + base, S, tid);
+    kst.load(kblock0);
+    if constexpr (!L::OVL) {
+        kst.store(smem, kscale, tid);
+        __syncthreads();
+        read_k();
+        __syncthreads();
     }
-    __syncthreads();
-    stage_block<D, KPW * NK, NT>(smem, V + base, S, kblock0, 1.f, tid);
-    __syncthreads();
+    vst.load(kblock0);
+    if constexpr (!L::OVL) {
+        vst.store(smem, 1.f, tid);
+        __syncthreads();
+        read_v();
+        __syncthreads();
+    }
+#endif
     if constexpr (M16) {
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int ks = 0; ks < D / 32; ++ks) st16.vf[nb][ks] = fo16.rowop(smem, wave * KPW + 16 * nb, ks);
 #pragma unroll
         for (int md = 0; md < D / 16; ++md)
 #pragma unroll
@@ -748,14 +787,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
                 st16.dka[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
                 st16.dva[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-    } else {
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-            for (int t = 0; t < D / 16; ++t) st.vf[kb][t] = fo.rowop(smem, wave * KPW + kb * 32, t);
     }
-    __syncthreads();
-#endif
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
 #if !FA2_BWD_COAL
@@ -843,6 +875,16 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
         dos.load(0);
     }
     load_rows(0);
+#if FA2_BWD_COAL
+    if constexpr (L::OVL) {
+        kst.store(smem, kscale, tid);
+        vst.store(vblk, 1.f, tid);
+        __syncthreads();
+        read_k();
+        read_v();
+        __syncthreads();
+    }
+#endif
     store_step(smem, smem + QS * TILE, 0);
     __syncthreads();
     // the group's tile within each staged image: folded into the per-lane offsets
@@ -978,7 +1020,7 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
                         const float* __restrict__ dO, const float* __restrict__ LSE,
                         const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV,
                         int S FA2_STAMP_ARG) {
-    __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, QS>::BYTES];
+    __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, KB, QS>::BYTES];
     dkdv_body<D, NW, KB, ABL, M16, QS>(lds, xcd_remap(blockIdx.x, gridDim.x), blockIdx.x, Q, K, V, dO, LSE, Delta, dK,
                                        dV, S FA2_STAMP_PASS);
 }
@@ -1104,7 +1146,12 @@ struct DqLds {
     static constexpr int KT = 32 * NKB, TILE = KT * D, NQ = NW / KS;
     // key-split merge records: per wave of groups 1..KS-1, dQᵀ (D / 2 floats per lane)
     static constexpr int MERGE = KS > 1 ? 2 * (KS - 1) * NQ * (D / 2) * 64 : 0;  // in halves
-    static constexpr int SMEM0 = (4 * KS * TILE > 32 * NQ * D) ? 4 * KS * TILE : 32 * NQ * D;
+    // OVL: the prologue's Q and dO blocks behind the first K/V buffer, loaded together
+    // with the first K/V step (small grids and D = 128, where the prologue's round
+    // trips are exposed; on the unsplit C3 grid it measured -1.7 %)
+    static constexpr bool OVL = KS > 1 || D == 128;
+    static constexpr int QD = OVL ? 2 * KS * TILE + 2 * 32 * NQ * D : 32 * NQ * D;
+    static constexpr int SMEM0 = 4 * KS * TILE > QD ? 4 * KS * TILE : QD;
     static constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;  // halves
     static constexpr int OSTAGE = 2 * SMEM;                     // byte offsets
     static constexpr int DBLK = OSTAGE + (FA2_BWD_COAL ? NQ * 32 * 36 * 4 : 0);
@@ -1149,34 +1196,78 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     FragOffsets16<D> fo16;
     const int g16 = lane >> 4, i16 = lane & 15;
     if constexpr (M16) fo16.init(lane);
+    // K/V staging by the first FA2_DQ_SW waves (all when 0), as in the dK/dV kernel
+    constexpr int SW = (FA2_DQ_SW > 0 && FA2_DQ_SW < NW) ? FA2_DQ_SW : NW;
+    TileStager<D, KT * KS, 64 * SW> ks, vs;
+    ks.init(K + base, S, tid);
+    vs.init(V + base, S, tid);
+    ks.on = vs.on = __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
+    const int ntiles = (S + KT - 1) / KT;
+    const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
+    const int nsteps = (ntiles + KS - 1) / KS;
 #if FA2_BWD_COAL
-    stage_block<D, 32 * NQ, NT>(smem, Q + base, S, qb * 32 * NQ, qscale, tid);
-    __syncthreads();
-    if constexpr (M16) {
+    // Prologue.  L::OVL: the Q and dO blocks (and O for Δ) and the first K/V step are
+    // loaded in one go (one HBM round trip instead of three), Q and dO in the second
+    // K/V buffer, which the first loop step restages only after the barrier below;
+    // else Q, then dO, then the first K/V step, each a round trip.
+    constexpr bool OVL = L::OVL;
+    _Float16* const qblk = OVL ? smem + 2 * KS * TILE : smem;
+    _Float16* const dblk = OVL ? qblk + 32 * NQ * D : smem;
+    auto read_q = [&] {
+        if constexpr (M16) {
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+            for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-            for (int ks = 0; ks < D / 32; ++ks) st16.qf[nb][ks] = fo16.rowop(smem, wave * 32 + 16 * nb, ks);
-    } else {
+                for (int ks = 0; ks < D / 32; ++ks) st16.qf[nb][ks] = fo16.rowop(qblk, wave * 32 + 16 * nb, ks);
+        } else {
 #pragma unroll
-        for (int t = 0; t < D / 16; ++t) st.qf[t] = fo.rowop(smem, wave * 32, t);
+            for (int t = 0; t < D / 16; ++t) st.qf[t] = fo.rowop(qblk, wave * 32, t);
+        }
+    };
+    auto read_d = [&] {
+        if constexpr (M16) {
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int ks = 0; ks < D / 32; ++ks) st16.df[nb][ks] = fo16.rowop(dblk, wave * 32 + 16 * nb, ks);
+        } else {
+#pragma unroll
+            for (int t = 0; t < D / 16; ++t) st.df[t] = fo.rowop(dblk, wave * 32, t);
+        }
+    };
+    {
+        using TS = TileStager<D, 32 * NQ, NT>;
+        TS qst, dst, ost;
+        qst.init(Q + base, S, tid);
+        dst.init(dO + base, S, tid);
+        qst.load(qb * 32 * NQ);
+        if constexpr (!OVL) {
+            qst.store(qblk, qscale, tid);
+            __syncthreads();
+            read_q();
+            __syncthreads();
+        }
+        dst.load(qb * 32 * NQ);
+        if (DELTA) {
+            ost.init(O + base, S, tid);
+            ost.load(qb * 32 * NQ);
+        }
+        if constexpr (OVL) {
+            ks.load(0);
+            vs.load(0);
+            qst.store(qblk, qscale, tid);
+        }
+        dst.store(dblk, 1.f, tid);
+        if (DELTA) delta_rows<D, 32 * NQ, NT>(dst, ost, S, qb * 32 * NQ, delta_blk, Delta + (long)bh * S, tid);
+        if constexpr (OVL) {
+            ks.store(smem, 1.f, tid);
+            vs.store(smem + KS * TILE, 1.f, tid);
+        }
+        __syncthreads();
+        if constexpr (OVL) read_q();
+        read_d();
+        if constexpr (!OVL) __syncthreads();
     }
-    __syncthreads();
-    if (DELTA)
-        stage_block_delta<D, 32 * NQ, NT>(smem, dO + base, O + base, S, qb * 32 * NQ, delta_blk,
-                                          Delta + (long)bh * S, tid);
-    else stage_block<D, 32 * NQ, NT>(smem, dO + base, S, qb * 32 * NQ, 1.f, tid);
-    __syncthreads();
-    if constexpr (M16) {
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int ks = 0; ks < D / 32; ++ks) st16.df[nb][ks] = fo16.rowop(smem, wave * 32 + 16 * nb, ks);
-    } else {
-#pragma unroll
-        for (int t = 0; t < D / 16; ++t) st.df[t] = fo.rowop(smem, wave * 32, t);
-    }
-    __syncthreads();
 #else
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
@@ -1216,21 +1307,13 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) st16.dqa[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-
-    // K/V staging by the first FA2_DQ_SW waves (all when 0), as in the dK/dV kernel
-    constexpr int SW = (FA2_DQ_SW > 0 && FA2_DQ_SW < NW) ? FA2_DQ_SW : NW;
-    TileStager<D, KT * KS, 64 * SW> ks, vs;
-    ks.init(K + base, S, tid);
-    vs.init(V + base, S, tid);
-    ks.on = vs.on = __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
     if (FA2_DQ_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(tid >> 6) >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    const int ntiles = (S + KT - 1) / KT;
-    const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
-    const int nsteps = (ntiles + KS - 1) / KS;
-    ks.load(0);
-    vs.load(0);
-    ks.store(smem, 1.f, tid);
-    vs.store(smem + KS * TILE, 1.f, tid);
+    if (!FA2_BWD_COAL || !L::OVL) {
+        ks.load(0);
+        vs.load(0);
+        ks.store(smem, 1.f, tid);
+        vs.store(smem + KS * TILE, 1.f, tid);
+    }
     __syncthreads();
     // the group's tile within each staged image: folded into the per-lane offsets
     if (KS > 1) fo16.shift(kg * TILE);
@@ -1360,21 +1443,21 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 // share nothing, so they run side by side on the chip instead of one kernel after
 // the other, and the second launch's ramp-up and tail go away.  Δ comes from a
 // prior fa2_delta_kernel (the dQ role cannot hand its fused Δ to the dK/dV role
-// without a cross-workgroup wait).  Both roles run 8 waves on the 16x16x32 path;
+// without a cross-workgroup wait).  Both roles run NW waves on the 16x16x32 path;
 // the LDS block is the larger of the two layouts, registers the larger of the two.
-template <int D, int QS, int KS, int NKB>
-__global__ void __launch_bounds__(512)
+template <int D, int NW, int QS, int KS, int NKB>
+__global__ void __launch_bounds__(64 * NW)
 fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                          const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
                          float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV, int S, int ndk) {
-    constexpr int B1 = DkdvLds<D, 8, QS>::BYTES, B2 = DqLds<D, 8, false, NKB, KS>::BYTES;
+    constexpr int B1 = DkdvLds<D, NW, 1, QS>::BYTES, B2 = DqLds<D, NW, false, NKB, KS>::BYTES;
     __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
     const int b = blockIdx.x;
     if (b < ndk)
-        dkdv_body<D, 8, 1, 0, true, QS>(lds, xcd_remap(b, ndk), b, Q, K, V, dO, LSE, Delta, dK, dV, S);
+        dkdv_body<D, NW, 1, 0, true, QS>(lds, xcd_remap(b, ndk), b, Q, K, V, dO, LSE, Delta, dK, dV, S);
     else
-        dq_body<D, 8, false, NKB, true, KS>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
-                                            const_cast<float*>(Delta), dQ, S, nullptr);
+        dq_body<D, NW, false, NKB, true, KS>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
+                                             const_cast<float*>(Delta), dQ, S, nullptr);
 }
 #endif
 
@@ -1776,14 +1859,14 @@ hipError_t FA2_TILE_LAUNCH(launch_bwd_dq_delta)(int D, const float* q, const flo
 
 namespace {
 #ifndef FA2_STAMPS
-template <int D, int QS, int KS, int NKB>
+template <int D, int NW, int QS, int KS, int NKB>
 hipError_t fused_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                         const float* delta, float* dq, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-    const long ndk = (long)bh * ((S + 32 * (8 / QS) - 1) / (32 * (8 / QS)));
-    const long ndq = (long)bh * ((S + 32 * (8 / KS) - 1) / (32 * (8 / KS)));
+    const long ndk = (long)bh * ((S + 32 * (NW / QS) - 1) / (32 * (NW / QS)));
+    const long ndq = (long)bh * ((S + 32 * (NW / KS) - 1) / (32 * (NW / KS)));
     if (ndk <= 0 || ndq <= 0 || ndk + ndq > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_fused_f16_kernel<D, QS, KS, NKB>), dim3((unsigned)(ndk + ndq)), dim3(512), 0,
-                       stream, q, k, v, dout, lse, delta, dq, dk, dv, S, (int)ndk);
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_fused_f16_kernel<D, NW, QS, KS, NKB>), dim3((unsigned)(ndk + ndq)),
+                       dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, dk, dv, S, (int)ndk);
     return hipGetLastError();
 }
 #endif
@@ -1800,11 +1883,24 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
     if constexpr (D > 64) {
         return hipErrorNotSupported;
     } else {
-        const int a = auto_waves((long)bh * ((S + 31) / 32), 8);
-        const int fqs = tune_knob("BWD_FQS", a == 8 ? 1 : 2), fks = tune_knob("BWD_FKS", a == 8 ? 1 : a == 4 ? 2 : 4);
-        if (fqs == 1 && fks == 1) return fused_launch<D, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
-        if (fqs == 2 && fks == 2) return fused_launch<D, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
-        if (fqs == 2 && fks == 4) return fused_launch<D, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        const long units = (long)bh * ((S + 31) / 32);
+        const int a = auto_waves(units, 8);
+        // below 2 blocks per CU: 4-wave roles, KS = 2 (B2_H8_S512: bwd 16.7 -> 15.7 us;
+        // at 2 blocks per CU, B2_H8_S1024, that geometry is 21 % slower than 8 waves)
+        const bool tiny = a == 2 && auto_waves(units, 2, 1) == 1;
+        const int fqs = tune_knob("BWD_FQS", a == 8 ? 1 : 2);
+        const int fks = tune_knob("BWD_FKS", a == 8 ? 1 : (a == 4 || tiny) ? 2 : 4);
+        // FA2_TUNE_BWD_FNW: waves per workgroup of both roles (8, or 4 for the split pairs)
+        const int fnw = tune_knob("BWD_FNW", tiny ? 4 : 8);
+        if (fqs == 1 && fks == 1) return fused_launch<D, 8, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        if (fnw == 4) {
+            if (fqs == 2 && fks == 2)
+                return fused_launch<D, 4, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+            if (fqs == 2 && fks == 4)
+                return fused_launch<D, 4, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        }
+        if (fqs == 2 && fks == 2) return fused_launch<D, 8, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        if (fqs == 2 && fks == 4) return fused_launch<D, 8, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
         return hipErrorNotSupported;
     }
 #endif

@@ -594,7 +594,10 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     constexpr int MREC = (D / 2 + 2) * 64;
     constexpr int MERGE = KS > 1 ? 2 * (KS - 1) * NQ * MREC : 0;  // in halves
     // [slot][K | V][KS] tiles; at least one Q block (coalesced prologue) and the merge
-    constexpr int SMEM0 = (2 * NSLOT * KS * TILE > 32 * MQ * NQ * D) ? 2 * NSLOT * KS * TILE : 32 * MQ * NQ * D;
+    // OVL: the prologue's Q block behind the first K/V buffer, loaded with the first step
+    constexpr bool OVL = KS > 1;
+    constexpr int QB = (OVL ? 2 * KS * TILE : 0) + 32 * MQ * NQ * D;
+    constexpr int SMEM0 = 2 * NSLOT * KS * TILE > QB ? 2 * NSLOT * KS * TILE : QB;
     constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;
     __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
 #if FA2_FWD_COAL
@@ -613,28 +616,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     FwdState<D> st[MQ];
     FragOffsets<D> fo;
     fo.init(lane);
-#if FA2_FWD_COAL
-    // Q block (32*MQ*NW rows, one contiguous HBM range) loaded row-coalesced, converted
-    // and scaled into the (still idle) K/V LDS buffers, then read back as this wave's
-    // B fragments: 1 KB per load instruction instead of 32 rows x 32 B per-lane pieces.
-    {
-        TileStager<D, 32 * MQ * NQ, NT> qst;
-        qst.init(Q + base, S, tid);
-        qst.load(qb * QW * NQ);
-        qst.store(smem, FA2_LOG2E / __builtin_sqrtf((float)D), tid);
-        __syncthreads();
-#pragma unroll
-        for (int g = 0; g < MQ; ++g) {
-            fwd_init<D, SEED>(st[g], nullptr, 0, S, S, h);  // state only (q >= S: no Q read)
-#pragma unroll
-            for (int t = 0; t < D / 16; ++t) st[g].qf[t] = fo.rowop(smem, wave * QW + 32 * g, t);
-        }
-        __syncthreads();
-    }
-#else
-#pragma unroll
-    for (int g = 0; g < MQ; ++g) fwd_init<D, SEED>(st[g], Q, base, q0 + 32 * g, S, h);
-#endif
     // K/V staging by the first FA2_FWD_SW waves (all when 0): the second half loses
     // VALU arbitration to its SIMD partners, so the first half takes the staging
     constexpr int SW = (FA2_FWD_SW > 0 && FA2_FWD_SW < NW) ? FA2_FWD_SW : NW;
@@ -646,14 +627,56 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     const int ntiles = (ABL & 64) ? 1 : (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     const int nsteps = (ntiles + KS - 1) / KS;
+#if FA2_FWD_COAL
+    // Q block (32*MQ*NW rows, one contiguous HBM range) loaded row-coalesced, converted
+    // and scaled into LDS, then read back as this wave's B fragments: 1 KB per load
+    // instruction instead of 32 rows x 32 B per-lane pieces.  OVL (key split: small
+    // grids, where the prologue's round trips are exposed): its loads and the first K/V
+    // step's go out together, Q behind the first K/V buffer; else Q first, through the
+    // (still idle) K/V buffers.
+    {
+        _Float16* const qblk = OVL ? smem + 2 * KS * TILE : smem;
+        TileStager<D, 32 * MQ * NQ, NT> qst;
+        qst.init(Q + base, S, tid);
+        qst.load(qb * QW * NQ);
+        if constexpr (OVL) {
+            ks.load(0);
+            vs.load(0);
+        }
+        qst.store(qblk, FA2_LOG2E / __builtin_sqrtf((float)D), tid);
+        if constexpr (OVL) {
+            ks.store(smem, 1.f, tid);
+            vs.store(smem + KS * TILE, 1.f, tid);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < MQ; ++g) {
+            fwd_init<D, SEED>(st[g], nullptr, 0, S, S, h);  // state only (q >= S: no Q read)
+#pragma unroll
+            for (int t = 0; t < D / 16; ++t) st[g].qf[t] = fo.rowop(qblk, wave * QW + 32 * g, t);
+        }
+        __syncthreads();  // every wave has its Q fragments before their buffer is restaged
+    }
     // the group's tile within each staged image: folded into the per-lane offsets, so
     // every LDS read keeps a compile-time tile base
+    if (KS > 1) fo.shift(kg * TILE);
+    if constexpr (!OVL) {
+        ks.load(0);
+        vs.load(0);
+        ks.store(smem, 1.f, tid);
+        vs.store(smem + KS * TILE, 1.f, tid);
+        __syncthreads();
+    }
+#else
+#pragma unroll
+    for (int g = 0; g < MQ; ++g) fwd_init<D, SEED>(st[g], Q, base, q0 + 32 * g, S, h);
     if (KS > 1) fo.shift(kg * TILE);
     ks.load(0);
     vs.load(0);
     ks.store(smem, 1.f, tid);
     vs.store(smem + KS * TILE, 1.f, tid);
     __syncthreads();
+#endif
 
     if (FA2_FWD_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
     if constexpr (STAG) {

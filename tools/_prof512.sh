@@ -1,0 +1,18 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/p512
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/p512 -o run -- python3 tools/kbench.py --shape 2,8,512,64 --kernel stepb --do ones --rounds 2 --iters 20 > gpurun_out/p512/kb.log 2>&1 || exit $?
+f=$(find gpurun_out/p512 -name "*kernel_trace.csv" | head -1)
+python3 - "$f" > gpurun_out/p512/gaps.txt <<'PY'
+import csv,sys
+rows=list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r:int(r["Start_Timestamp"]))
+rows=[r for r in rows if "fa2" in r["Kernel_Name"] or "delta" in r["Kernel_Name"]]
+last=rows[-60:]
+prev=None
+for r in last:
+    s,e=int(r["Start_Timestamp"]),int(r["End_Timestamp"])
+    gap=(s-prev)/1000 if prev else 0
+    print(f"{r['Kernel_Name'][:70]:70s} dur {(e-s)/1000:7.2f} us gap {gap:6.2f} grid {r.get('Grid_Size','')} wg {r.get('Workgroup_Size','')} lds {r.get('LDS_Block_Size', r.get('Lds_Size',''))}")
+    prev=e
+PY
