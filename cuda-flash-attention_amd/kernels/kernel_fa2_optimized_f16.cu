@@ -44,6 +44,7 @@ namespace fa2f16 {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
@@ -67,8 +68,20 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
 }
+// sum of a packed pair of tile values plus c (v_dot2_f32_bf16 against ones)
+__device__ __forceinline__ float pair_sum(_Float16 a, _Float16 b, float c) {
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const s16x2 v = {__builtin_bit_cast(short, a), __builtin_bit_cast(short, b)};
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v), bf16x2{(__bf16)1.f, (__bf16)1.f}, c, false);
+}
 #else
 __device__ __forceinline__ _Float16 to_tile(float x) { return (_Float16)x; }
+// sum of a packed pair of tile values plus c (v_dot2_f32_f16 against ones)
+__device__ __forceinline__ float pair_sum(_Float16 a, _Float16 b, float c) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_fdot2(f16x2{a, b}, f16x2{(_Float16)1.f, (_Float16)1.f}, c, false);
+}
 __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
@@ -318,8 +331,53 @@ __device__ __forceinline__ float tile_max(const f32x16 (&t)[NKB]) {
 }
 
 // p = exp2(s - m - sh) of the tile, packed to fp16, with its four partial row sums.
+// FA2_FWD_PKSUM: the four partial row sums as 0 = scalar f32 adds (one issue per
+// score), 1 = two float2 chains (v_pk_add_f32; at C3 the pairing spilled 15 VGPRs),
+// 2 = v_dot2 of the packed tile values against ones (one issue per two scores).
+#ifndef FA2_FWD_PKSUM
+#define FA2_FWD_PKSUM 2
+#endif
 template <bool SHIFT, int ABL = 0, int NKB = 2>
 __device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[NKB], float sh, f16x8 (&pf)[NKB][2], float (&ls)[4]) {
+#if FA2_FWD_PKSUM == 2
+    // the row sums from the packed fp16 probabilities (v_dot2 against ones: one issue
+    // per two scores, and l sums exactly the P the PV MFMAs multiply)
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float x = SHIFT ? sacc[kb][i] - sh : sacc[kb][i];
+            const float p = (ABL & 2) ? x : fast_exp2(x);
+            pf[kb][i >> 3][i & 7] = to_tile(p);
+        }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ls[c] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = (kb * 8 + j) & 3;
+            ls[c] = pair_sum(pf[kb][j >> 2][2 * (j & 3)], pf[kb][j >> 2][2 * (j & 3) + 1], ls[c]);
+        }
+#elif FA2_FWD_PKSUM
+    f32x2 acc[2];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+            f32x2 x = {sacc[kb][i], sacc[kb][i + 1]};
+            if (SHIFT) x -= sh;
+            const f32x2 p = (ABL & 2) ? x : f32x2{fast_exp2(x[0]), fast_exp2(x[1])};
+            if (kb == 0 && i < 4) acc[i >> 1] = p;
+            else acc[(i >> 1) & 1] += p;
+            pf[kb][i >> 3][i & 7] = to_tile(p[0]);
+            pf[kb][i >> 3][(i & 7) + 1] = to_tile(p[1]);
+        }
+    ls[0] = acc[0][0];
+    ls[1] = acc[0][1];
+    ls[2] = acc[1][0];
+    ls[3] = acc[1][1];
+#else
 #pragma unroll
     for (int c = 0; c < 4; ++c) ls[c] = 0.f;
 #pragma unroll
@@ -331,6 +389,7 @@ __device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[NKB], float sh, f16
             ls[i & 3] += p;
             pf[kb][i >> 3][i & 7] = to_tile(p);
         }
+#endif
 }
 
 // Online softmax of one tile for the wave's MQ query groups (sacc = s - m) and
