@@ -78,6 +78,26 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 #endif
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// dS = P * (dP - Δ) for a pair of scores, as tile values.  FA2_DS_PK (fp16 tiles):
+// the product of the already-packed fp16 P and the packed (dP - Δ) (v_cvt_pk +
+// v_pk_mul_f16: one issue per score fewer than two f32 products and a conversion);
+// else the f32 products, rounded once.
+#ifndef FA2_DS_PK
+#define FA2_DS_PK 1
+#endif
+typedef _Float16 tile2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ tile2 ds_pair(float p0, float p1, float d0, float d1, _Float16 ph0, _Float16 ph1) {
+#if FA2_DS_PK && !defined(FA2_TILE_BF16)
+    (void)p0;
+    (void)p1;
+    return tile2{ph0, ph1} * tile2{(_Float16)d0, (_Float16)d1};
+#else
+    (void)ph0;
+    (void)ph1;
+    return tile2{to_tile(p0 * d0), to_tile(p1 * d1)};
+#endif
+}
+
 template <int D> struct Swz;
 // XOR swizzle of the 16-byte chunk index of LDS row r, searched (tools/lds_swizzle.py,
 // `swz_shipped`) to make ds_read_b128 row fragments and ds_read_b64_tr_b16 transposed
@@ -509,15 +529,21 @@ __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* 
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float sv = sa[j >> 2][nb][j & 3], dvv = da[j >> 2][nb][j & 3];
+            for (int j = 0; j < 8; j += 2) {
+                const float sv0 = sa[j >> 2][nb][j & 3], dv0 = da[j >> 2][nb][j & 3];
+                const float sv1 = sa[j >> 2][nb][(j & 3) + 1], dv1 = da[j >> 2][nb][(j & 3) + 1];
                 if (ABL & 2) {
-                    pf[nb][j] = to_tile(sv);
-                    dsf[nb][j] = to_tile(dvv);
+                    pf[nb][j] = to_tile(sv0);
+                    pf[nb][j + 1] = to_tile(sv1);
+                    dsf[nb][j] = to_tile(dv0);
+                    dsf[nb][j + 1] = to_tile(dv1);
                 } else {
-                    const float pv = fast_exp2(sv);
-                    pf[nb][j] = to_tile(pv);
-                    dsf[nb][j] = to_tile(pv * dvv);
+                    const float p0 = fast_exp2(sv0), p1 = fast_exp2(sv1);
+                    pf[nb][j] = to_tile(p0);
+                    pf[nb][j + 1] = to_tile(p1);
+                    const tile2 d2 = ds_pair(p0, p1, dv0, dv1, pf[nb][j], pf[nb][j + 1]);
+                    dsf[nb][j] = d2[0];
+                    dsf[nb][j + 1] = d2[1];
                 }
             }
         if (ABL & 8) {
@@ -583,10 +609,14 @@ __device__ __forceinline__ void dkdv16_soft(const Dkdv16Blk<D>& b, f16x8 (&pf)[2
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float pv = fast_exp2(b.sa[j >> 2][nb][j & 3]);
-            pf[nb][j] = to_tile(pv);
-            dsf[nb][j] = to_tile(pv * b.da[j >> 2][nb][j & 3]);
+        for (int j = 0; j < 8; j += 2) {
+            const float p0 = fast_exp2(b.sa[j >> 2][nb][j & 3]), p1 = fast_exp2(b.sa[j >> 2][nb][(j & 3) + 1]);
+            pf[nb][j] = to_tile(p0);
+            pf[nb][j + 1] = to_tile(p1);
+            const tile2 d2 = ds_pair(p0, p1, b.da[j >> 2][nb][j & 3], b.da[j >> 2][nb][(j & 3) + 1], pf[nb][j],
+                                     pf[nb][j + 1]);
+            dsf[nb][j] = d2[0];
+            dsf[nb][j + 1] = d2[1];
         }
 }
 
