@@ -410,10 +410,10 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
     }
     f16x8 pf[MQ][NKB][2];
     float ls[MQ][4];
-    // l += tile sums, O^T += V^T P^T.  Issued inside each branch (64-key tiles): joining
-    // the paths before it made the register allocator copy O and l (29 v_mov per tile
-    // on the common path, r01 ISA audit); joined after it, the merged values are MFMA
-    // results.  32-key tiles (D = 128 at 8 waves) join first: the duplicate spills.
+    // l += tile sums, O^T += V^T P^T.  Issued inside each branch: joining the paths
+    // before it made the register allocator copy O and l on the common path (r01 ISA
+    // audit: 29 v_mov per 64-key tile at D = 64; 32 v_mov_b64 + 5 v_mov_b32 per 32-key
+    // tile at D = 128); joined after it, the merged values are MFMA results.
     auto accumulate = [&]() {
 #pragma unroll
         for (int g = 0; g < MQ; ++g)
@@ -460,11 +460,10 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
             if (SEED) st[g].nm = splat16(-st[g].m);
             fwd_exp<true, ABL, NKB>(sacc[g], SEED ? d : st[g].m, pf[g], ls[g]);
         }
-        if (NKB == 2) accumulate();
-    } else if (NKB == 2) {
+        accumulate();
+    } else {
         accumulate();
     }
-    if (NKB != 2) accumulate();
 }
 
 template <int D, bool SEED = true>
