@@ -945,18 +945,22 @@ __device__ __forceinline__ void fwd16_tile(Fwd16State<D>& st, const _Float16* Ks
     }
     f16x8 pf[NKB][2];  // [32-key step][nb]
     float ls[2];
+    // p = exp2(s - sh) packed to fp16; the row sums by v_dot2 of the packed pairs (as in
+    // fwd_exp, FA2_FWD_PKSUM = 2), two chains per 16-query block
     auto expo = [&](float sh) {
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
+#pragma unroll
+            for (int kq = 0; kq < NKB; ++kq)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pf[kq][nb][j] = to_tile(fast_exp2(sa[2 * kq + (j >> 2)][nb][j & 3] - sh));
             float a0 = 0.f, a1 = 0.f;
 #pragma unroll
             for (int kq = 0; kq < NKB; ++kq)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float pv = fast_exp2(sa[2 * kq + (j >> 2)][nb][j & 3] - sh);
-                    if (j & 1) a1 += pv;
-                    else a0 += pv;
-                    pf[kq][nb][j] = to_tile(pv);
+                for (int j = 0; j < 8; j += 2) {
+                    if ((j >> 1) & 1) a1 = pair_sum(pf[kq][nb][j], pf[kq][nb][j + 1], a1);
+                    else a0 = pair_sum(pf[kq][nb][j], pf[kq][nb][j + 1], a0);
                 }
             ls[nb] = a0 + a1;
         }
@@ -1002,24 +1006,24 @@ __device__ __forceinline__ void fwd16_tile(Fwd16State<D>& st, const _Float16* Ks
         // p relative to the new m (sa holds s - m_old); two shifts as one expo pass
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
+#pragma unroll
+            for (int kq = 0; kq < NKB; ++kq)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pf[kq][nb][j] = to_tile(fast_exp2(sa[2 * kq + (j >> 2)][nb][j & 3] - dd[nb]));
             float a0 = 0.f, a1 = 0.f;
 #pragma unroll
             for (int kq = 0; kq < NKB; ++kq)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float pv = fast_exp2(sa[2 * kq + (j >> 2)][nb][j & 3] - dd[nb]);
-                    if (j & 1) a1 += pv;
-                    else a0 += pv;
-                    pf[kq][nb][j] = to_tile(pv);
+                for (int j = 0; j < 8; j += 2) {
+                    if ((j >> 1) & 1) a1 = pair_sum(pf[kq][nb][j], pf[kq][nb][j + 1], a1);
+                    else a0 = pair_sum(pf[kq][nb][j], pf[kq][nb][j + 1], a0);
                 }
             ls[nb] = a0 + a1;
         }
-        if (NKB == 2) pv_acc();
-    } else if (NKB == 2) {
         pv_acc();
+    } else {
+        pv_acc();  // inside both branches: a join before it copies O on the common path
     }
-    // 32-key tiles (D = 128 at 8 waves): one PV after the join (duplicated, it spills)
-    if (NKB != 2) pv_acc();
 }
 
 template <int D, int NW, int NKB>
