@@ -1240,7 +1240,11 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     TileStager<D, KT * KS, 64 * SW> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
-    ks.on = vs.on = __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
+    // Staging flag compile-time true at D = 128 (all waves stage): the runtime flag's
+    // branches around the loads left 34 v_mov_b64 of staging-register copies there (dQ
+    // +11.8 % without).  At D <= 64 the runtime flag stays: with it gone the compiler
+    // schedules the mid-tile loads differently and dQ ran 4.5 % slower at C3.
+    ks.on = vs.on = (SW == NW && D > 64) || __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
     const int ntiles = (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     const int nsteps = (ntiles + KS - 1) / KS;

@@ -681,7 +681,9 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     TileStager<D, KT * KS, 64 * SW> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
-    ks.on = vs.on = __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
+    // (compile-time true when all waves stage: fewer branches around the loads, +0.7 %
+    // at C3, +1.9 % at C4)
+    ks.on = vs.on = SW == NW || __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
     const int ntiles = (ABL & 64) ? 1 : (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     const int nsteps = (ntiles + KS - 1) / KS;
