@@ -404,6 +404,10 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
 #endif
 // FA2_*_PRIO: s_setprio 1 for waves 4-7 of 8-wave workgroups (the second-dispatched
 // half loses VALU arbitration by age; MI355X_MICROARCH §Two waves per SIMD, item 4)
+// FA2_DKDV_QM_SW: staging waves of the QM > 1 instances (0 = all)
+#ifndef FA2_DKDV_QM_SW
+#define FA2_DKDV_QM_SW 0
+#endif
 #ifndef FA2_DKDV_PRIO
 #define FA2_DKDV_PRIO 0
 #endif
@@ -708,9 +712,9 @@ __device__ __forceinline__ void store_block_rows16(float (*os)[36], const f32x4 
 // The workgroup's LDS: [buf][Q | dO][QS] fp16 tiles (or the query-split merge
 // records), [buf][-lse2 | -delta][QS] fp32 rows, the per-wave result stage.  Carved
 // from one block so the fused backward kernel can overlay it with the dQ role's.
-template <int D, int NW, int KB, int QS>
+template <int D, int NW, int KB, int QS, int QM = 1>
 struct DkdvLds {
-    static constexpr int QT = 64, TILE = QT * D, NK = NW / QS;
+    static constexpr int QT = 64, TILE = QT * D, NK = NW / QS, TPS = QS * QM;
     // query-split merge records: per wave of groups 1..QS-1, dKᵀ and dVᵀ (D floats per lane)
     static constexpr int MERGE = QS > 1 ? 2 * (QS - 1) * NK * D * 64 : 0;  // in halves
     // OVL: the prologue's K and V blocks side by side, loaded together with the first
@@ -718,22 +722,27 @@ struct DkdvLds {
     // unsplit C3 grid it measured -1.2 %)
     static constexpr bool OVL = QS > 1;
     static constexpr int KV = OVL ? 2 * 32 * KB * NK * D : 0;
-    static constexpr int SMEM0 = 2 * 2 * QS * TILE > MERGE ? 2 * 2 * QS * TILE : MERGE;
+    static constexpr int SMEM0 = 2 * 2 * TPS * TILE > MERGE ? 2 * 2 * TPS * TILE : MERGE;
     static constexpr int SMEM = (FA2_BWD_COAL && KV > SMEM0) ? KV : SMEM0;  // halves
     static constexpr int ROWS = 2 * SMEM;                      // byte offsets
-    static constexpr int OSTAGE = ROWS + 2 * 2 * QS * QT * 4;
+    static constexpr int OSTAGE = ROWS + 2 * 2 * TPS * QT * 4;
     static constexpr int BYTES = OSTAGE + (FA2_BWD_COAL ? NK * 32 * 36 * 4 : 0);
 };
 
 // One workgroup of the dK/dV kernel; `bid` is its (XCD-remapped) block number over
 // the BH * ceil(S / (KPW * NK)) key blocks, `blk` the raw one (stamp records only).
-template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false, int QS = 1>
+template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false, int QS = 1, int QM = 1>
 __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int blk, const float* __restrict__ Q,
                                           const float* __restrict__ K, const float* __restrict__ V,
                                           const float* __restrict__ dO, const float* __restrict__ LSE,
                                           const float* __restrict__ Delta, float* __restrict__ dK,
                                           float* __restrict__ dV, int S FA2_STAMP_ARG) {
-    using L = DkdvLds<D, NW, KB, QS>;
+    using L = DkdvLds<D, NW, KB, QS, QM>;
+    // QM: query tiles per group per step (every wave of the group runs them one after
+    // the other: one barrier and one staging round per QM tiles).  The step's staged
+    // image holds TPS = QS * QM tiles; group g takes tiles g + QS * m.
+    constexpr int TPS = L::TPS;
+    static_assert(QM == 1 || (M16 && 2 * TPS <= NW && !FA2_STAMPS_ON), "QM > 1: 16x16x32, 2 TPS row waves");
     constexpr int QT = L::QT;  // query rows per step
     constexpr int NT = 64 * NW;
     constexpr int TILE = L::TILE;
@@ -741,7 +750,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
     static_assert(QS == 1 || (M16 && 2 * QS <= NW && !FA2_STAMPS_ON), "query split: 16x16x32, 2 QS row waves");
     constexpr int NK = L::NK;  // key waves (QS > 1: waves w, w + NK, ... share keys)
     _Float16* smem = reinterpret_cast<_Float16*>(lds);
-    float(*rows)[2][QS * QT] = reinterpret_cast<float(*)[2][QS * QT]>(lds + L::ROWS);
+    float(*rows)[2][TPS * QT] = reinterpret_cast<float(*)[2][TPS * QT]>(lds + L::ROWS);
 #if FA2_BWD_COAL
     float(*ostage)[32][36] = reinterpret_cast<float(*)[32][36]>(lds + L::OSTAGE);  // per-wave result stage
 #endif
@@ -850,11 +859,12 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
     // NW when 0): stamps showed waves NW/2..NW-1 (which lose VALU arbitration to their
     // SIMD partners) ~15 % slower per step and the first half idling at the barrier,
     // so the staging work goes to the first half.
-    constexpr int SW = (FA2_DKDV_SW > 0 && FA2_DKDV_SW < NW) ? FA2_DKDV_SW : NW;
+    constexpr int SW = QM > 1 ? (FA2_DKDV_QM_SW > 0 && FA2_DKDV_QM_SW < NW ? FA2_DKDV_QM_SW : NW)
+                              : (FA2_DKDV_SW > 0 && FA2_DKDV_SW < NW) ? FA2_DKDV_SW : NW;
     constexpr int NS = 64 * SW;
     const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool stg = wave_u < SW;
-    TileStager<D, QT * QS, NS> qs, dos;
+    TileStager<D, QT * TPS, NS> qs, dos;
     qs.init(Q + base, S, tid);
     dos.init(dO + base, S, tid);
     // Row constants of the staged step: wave 0 carries LSE, wave 1 carries Delta
@@ -870,34 +880,34 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
     const __amdgpu_buffer_rsrc_t rs_del = head_rsrc(Delta + rbase, S, 1);
     float rowraw = 0.f;
     int rowq = 0;
-    const int rw = wave_u % QS;  // which of the step's tiles this wave's row vector is
+    const int rw = wave_u % TPS;  // which of the step's tiles this wave's row vector is
     auto load_rows = [&](int q0) {
         q0 += rw * QT;
         rowq = q0 + lane;
-        if (wave_u < QS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
-        else if (wave_u < 2 * QS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_del, lane * 4, q0 * 4, 0));
+        if (wave_u < TPS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
+        else if (wave_u < 2 * TPS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_del, lane * 4, q0 * 4, 0));
     };
     auto store_rows = [&](int buf) {
         // stored negated: they are the initial accumulators of S and dP
-        if (wave_u < QS) rows[buf][0][rw * QT + lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
-        else if (wave_u < 2 * QS) rows[buf][1][rw * QT + lane] = -rowraw;
+        if (wave_u < TPS) rows[buf][0][rw * QT + lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
+        else if (wave_u < 2 * TPS) rows[buf][1][rw * QT + lane] = -rowraw;
     };
     // where the next step's global loads are issued (all eight waves issuing them at
     // once right after the barrier queue on the texture unit): FA2_DKDV_LP
     // 0 = all at the step start, 1 = all between the two query blocks, 2 = Q at the
     // start and dO + row constants between the blocks
     auto load_a = [&](int it) {
-        if ((FA2_DKDV_LP == 0 || FA2_DKDV_LP == 2) && stg) qs.load(it * QS * QT);
+        if ((FA2_DKDV_LP == 0 || FA2_DKDV_LP == 2) && stg) qs.load(it * TPS * QT);
         if (FA2_DKDV_LP == 0) {
-            if (stg) dos.load(it * QS * QT);
-            load_rows(it * QS * QT);
+            if (stg) dos.load(it * TPS * QT);
+            load_rows(it * TPS * QT);
         }
     };
     auto load_b = [&](int it) {
-        if (FA2_DKDV_LP == 1 && stg) qs.load(it * QS * QT);
+        if (FA2_DKDV_LP == 1 && stg) qs.load(it * TPS * QT);
         if (FA2_DKDV_LP != 0) {
-            if (stg) dos.load(it * QS * QT);
-            load_rows(it * QS * QT);
+            if (stg) dos.load(it * TPS * QT);
+            load_rows(it * TPS * QT);
         }
     };
     auto store_step = [&](_Float16* qdst, _Float16* ddst, int rbuf) {
@@ -908,7 +918,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
         store_rows(rbuf);
     };
     const int nqt = (S + QT - 1) / QT;  // query tiles
-    const int nsteps = (nqt + QS - 1) / QS;
+    const int nsteps = (nqt + TPS - 1) / TPS;
     if (stg) {
         qs.load(0);
         dos.load(0);
@@ -924,7 +934,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
         __syncthreads();
     }
 #endif
-    store_step(smem, smem + QS * TILE, 0);
+    store_step(smem, smem + TPS * TILE, 0);
     __syncthreads();
     // the group's tile within each staged image: folded into the per-lane offsets
     if (QS > 1) fo16.shift(qg * TILE);
@@ -934,47 +944,52 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
     unsigned long long stv[FA2_NSTAMP] = {0, 0, 0, 0, 0}, tprev;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
 #endif
+    // one staged step: the group's QM tiles g + QS m, each one dkdv_step16 (the next
+    // step's mid-step loads inside the first)
+    auto run_step = [&](const _Float16* Qb, const _Float16* dOb, const float* r0, const float* r1, int itc,
+                        auto&& mid) {
+        if constexpr (M16) {
+#pragma unroll
+            for (int m = 0; m < QM; ++m) {
+                const bool live = (QS == 1 && QM == 1) || itc * TPS + qg + QS * m < nqt;  // wave-uniform
+                if (!live) {
+                    if (m == 0) mid();
+                } else if (m == 0) {
+                    if (FA2_DKDV_PIPE && ABL == 0)
+                        dkdv_step16_pipe<D>(st16, Qb, dOb, r0 + rq, r1 + rq, fo16, g16, mid);
+                    else dkdv_step16<D, ABL>(st16, Qb, dOb, r0 + rq, r1 + rq, fo16, g16, mid);
+                } else {
+                    dkdv_step16<D, ABL>(st16, Qb + m * QS * TILE, dOb + m * QS * TILE, r0 + rq + m * QS * QT,
+                                        r1 + rq + m * QS * QT, fo16, g16, [] {});
+                }
+            }
+        } else {
+            dkdv_step<D, KB, ABL>(st, Qb, dOb, r0, r1, fo, h, mid);
+        }
+    };
     for (int it = 0; it < nsteps; it += 2) {
         {
             const bool more = !(ABL & 1) && it + 1 < nsteps;
-            const bool live = QS == 1 || it * QS + qg < nqt;  // wave-uniform
             if (more) load_a(it + 1);
             FA2_STAMP(0);
-            auto mid = [&] {
+            run_step(smem, smem + TPS * TILE, rows[0][0], rows[0][1], it, [&] {
                 if (more) load_b(it + 1);
-            };
-            if constexpr (M16) {
-                if (!live) mid();
-                else if (FA2_DKDV_PIPE && ABL == 0)
-                    dkdv_step16_pipe<D>(st16, smem, smem + QS * TILE, rows[0][0] + rq, rows[0][1] + rq, fo16, g16, mid);
-                else dkdv_step16<D, ABL>(st16, smem, smem + QS * TILE, rows[0][0] + rq, rows[0][1] + rq, fo16, g16, mid);
-            } else
-                dkdv_step<D, KB, ABL>(st, smem, smem + TILE, rows[0][0], rows[0][1], fo, h, mid);
+            });
             FA2_STAMP(1);
-            if (more) store_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, 1);
+            if (more) store_step(smem + 2 * TPS * TILE, smem + 3 * TPS * TILE, 1);
             FA2_STAMP(2);
             if (!(ABL & 4)) __syncthreads();
             FA2_STAMP(3);
         }
         if (it + 1 < nsteps) {
             const bool more = !(ABL & 1) && it + 2 < nsteps;
-            const bool live = QS == 1 || (it + 1) * QS + qg < nqt;
             if (more) load_a(it + 2);
             FA2_STAMP(0);
-            auto mid = [&] {
+            run_step(smem + 2 * TPS * TILE, smem + 3 * TPS * TILE, rows[1][0], rows[1][1], it + 1, [&] {
                 if (more) load_b(it + 2);
-            };
-            if constexpr (M16) {
-                if (!live) mid();
-                else if (FA2_DKDV_PIPE && ABL == 0)
-                    dkdv_step16_pipe<D>(st16, smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0] + rq,
-                                        rows[1][1] + rq, fo16, g16, mid);
-                else dkdv_step16<D, ABL>(st16, smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0] + rq,
-                                         rows[1][1] + rq, fo16, g16, mid);
-            } else
-                dkdv_step<D, KB, ABL>(st, smem + 2 * TILE, smem + 3 * TILE, rows[1][0], rows[1][1], fo, h, mid);
+            });
             FA2_STAMP(1);
-            if (more) store_step(smem, smem + QS * TILE, 0);
+            if (more) store_step(smem, smem + TPS * TILE, 0);
             FA2_STAMP(2);
             if (!(ABL & 4)) __syncthreads();
             FA2_STAMP(3);
@@ -1053,14 +1068,14 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
 #endif
 }
 
-template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false, int QS = 1>
+template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false, int QS = 1, int QM = 1>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                         const float* __restrict__ dO, const float* __restrict__ LSE,
                         const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV,
                         int S FA2_STAMP_ARG) {
-    __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, KB, QS>::BYTES];
-    dkdv_body<D, NW, KB, ABL, M16, QS>(lds, xcd_remap(blockIdx.x, gridDim.x), blockIdx.x, Q, K, V, dO, LSE, Delta, dK,
+    __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, KB, QS, QM>::BYTES];
+    dkdv_body<D, NW, KB, ABL, M16, QS, QM>(lds, xcd_remap(blockIdx.x, gridDim.x), blockIdx.x, Q, K, V, dO, LSE, Delta, dK,
                                        dV, S FA2_STAMP_PASS);
 }
 
@@ -1721,6 +1736,20 @@ hipError_t dkdv_launch_qs(const float* q, const float* k, const float* v, const 
 #endif
 }
 
+template <int D, int NW, int QM>
+hipError_t dkdv_launch_qm(const float* q, const float* k, const float* v, const float* dout, const float* lse,
+                          const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
+#ifdef FA2_STAMPS
+    return hipErrorNotSupported;
+#else
+    const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, 1, 0, true, 1, QM>), dim3((unsigned)grid),
+                       dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dk, dv, S);
+    return hipGetLastError();
+#endif
+}
+
 template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false>
 hipError_t dkdv_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                        const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
@@ -1797,8 +1826,12 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
         if (nw == 8) {
             // FA2_TUNE_DKDV_MF: MFMA shape, 16 (16x16x32, default: +5 % at C3 -- fewer
             // joules per FLOP under the power cap) or 32 (32x32x16)
-            if (tune_knob("DKDV_MF", 16) == 16)
+            if (tune_knob("DKDV_MF", 16) == 16) {
+                // FA2_TUNE_DKDV_QM: query tiles per step (2: one barrier and staging round
+                // per 128 queries)
+                if (tune_knob("DKDV_QM", 1) == 2) return dkdv_launch_qm<D, 8, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
                 return dkdv_launch<D, 8, 1, 0, true>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+            }
             return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
         }
     }
