@@ -70,7 +70,9 @@ int fa2_backward_dq(const float* q, const float* k, const float* v, const float*
                     const float* delta, float* dq, int batch, int heads, int seq, int head_dim, void* stream);
 /* dQ with Δ computed in the same kernel (from O and dO) and written to `delta`
  * (B*H*S floats); fa2_backward_dkdv launched after it reads that Δ.  This pair is
- * what fa2_backward runs for FA2_FP16 (fp16 tiles only). */
+ * what fa2_backward runs for FA2_FP16 / FA2_BF16 on grids of at least 8 blocks of 32
+ * rows per CU; on smaller grids (D <= 64) it runs fa2_delta and then ONE launch whose
+ * workgroups take the dK/dV or the dQ role side by side (FA2_TUNE_BWD_FUSED). */
 int fa2_backward_dq_delta(const float* q, const float* k, const float* v, const float* o, const float* dout,
                           const float* lse, float* delta, float* dq, int batch, int heads, int seq, int head_dim,
                           void* stream);
