@@ -243,19 +243,11 @@ struct TileStager {
 #define FA2_BWD_COAL 1
 #endif
 
-template <int D, int ROWS, int NT>
-__device__ __forceinline__ void stage_block(_Float16* lds, const float* head_base, int S, int row0, float scale,
-                                            int tid) {
-    TileStager<D, ROWS, NT> st;
-    st.init(head_base, S, tid);
-    st.load(row0);
-    st.store(lds, scale, tid);
-}
 
-// dO block -> fp16 LDS (as stage_block) and, fused, Δ = rowsum(dO ∘ O) of the
-// block's rows from the same row-coalesced registers: the CPR threads that hold one
-// row's chunks are consecutive lanes, reduced with xor shuffles.  Δ goes to
-// `delta_lds` (this workgroup's rows) and to HBM for the dK/dV kernel.
+// Δ = rowsum(dO ∘ O) of a staged block's rows, from the row-coalesced registers of
+// its dO and O stagers: the CPR threads that hold one row's chunks are consecutive
+// lanes, reduced with xor shuffles.  Δ goes to `delta_lds` (this workgroup's rows)
+// and to HBM for the dK/dV kernel.
 template <int D, int ROWS, int NT>
 __device__ __forceinline__ void delta_rows(const TileStager<D, ROWS, NT>& a, const TileStager<D, ROWS, NT>& o, int S,
                                            int row0, float* delta_lds, float* __restrict__ delta_out, int tid) {
@@ -273,18 +265,6 @@ __device__ __forceinline__ void delta_rows(const TileStager<D, ROWS, NT>& a, con
             if (row0 + row < S) delta_out[row0 + row] = d;
         }
     }
-}
-template <int D, int ROWS, int NT>
-__device__ __forceinline__ void stage_block_delta(_Float16* lds, const float* dO_head, const float* O_head, int S,
-                                                  int row0, float* delta_lds, float* __restrict__ delta_out,
-                                                  int tid) {
-    TileStager<D, ROWS, NT> a, o;
-    a.init(dO_head, S, tid);
-    o.init(O_head, S, tid);
-    a.load(row0);
-    o.load(row0);
-    a.store(lds, 1.f, tid);
-    delta_rows<D, ROWS, NT>(a, o, S, row0, delta_lds, delta_out, tid);
 }
 
 // a wave's 32 x D accumulator block (row d = 32b + (i&3) + 8(i>>2) + 4h of the
