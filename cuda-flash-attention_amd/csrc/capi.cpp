@@ -5,7 +5,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
 #include <cstdio>
 #include <string>
 #include <thread>
@@ -60,11 +63,20 @@ struct DevBuf {
 
 }  // namespace
 
+namespace {
+// launch-plan overrides set through fa2_tune_set (empty in production)
+std::mutex g_tune_mu;
+std::vector<std::pair<std::string, int>> g_tune;
+std::atomic<int> g_tune_n{0};
+}  // namespace
+
 namespace fa2 {
 int tune_knob(const char* name, int dflt) {
-    std::string key = std::string("FA2_TUNE_") + name;
-    const char* v = getenv(key.c_str());
-    return v ? atoi(v) : dflt;
+    if (g_tune_n.load(std::memory_order_acquire) == 0) return dflt;
+    std::lock_guard<std::mutex> lock(g_tune_mu);
+    for (const auto& kv : g_tune)
+        if (kv.first == name) return kv.second;
+    return dflt;
 }
 
 int auto_waves(long blocks32, int maxnw, int minnw) {
@@ -86,7 +98,22 @@ int auto_waves(long blocks32, int maxnw, int minnw) {
 
 extern "C" {
 
-int fa2_version(void) { return 1 * 10000 + 0 * 100 + 0; }
+int fa2_version(void) { return 1 * 10000 + 1 * 100 + 0; }
+
+int fa2_tune_set(const char* knob, int value) {
+    std::lock_guard<std::mutex> lock(g_tune_mu);
+    if (!knob) {
+        g_tune.clear();
+    } else {
+        if (!*knob || strlen(knob) > 32) return fail(FA2_E_INVALID, "bad knob name");
+        bool found = false;
+        for (auto& kv : g_tune)
+            if (kv.first == knob) kv.second = value, found = true;
+        if (!found) g_tune.emplace_back(knob, value);
+    }
+    g_tune_n.store((int)g_tune.size(), std::memory_order_release);
+    return FA2_OK;
+}
 
 const char* fa2_last_error(void) { return g_err.c_str(); }
 

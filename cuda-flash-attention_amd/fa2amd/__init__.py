@@ -34,7 +34,7 @@ SUPPORTED_HEAD_DIMS = (32, 64, 128)
 C_SYMBOLS = (
     "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv", "fa2_backward_dq", "fa2_backward_dq_delta",
     "fa2_naive_forward", "fa2_fa1_forward",
-    "fa2_forward_host", "fa2_backward_host", "fa2_shard_range", "fa2_last_error",
+    "fa2_forward_host", "fa2_backward_host", "fa2_shard_range", "fa2_tune_set", "fa2_last_error",
     "fa2_version", "fa2_device_count",
 )
 
@@ -93,6 +93,7 @@ def _load(path):
         "fa2_forward_host": [P] * 5 + [I] * 6 + [FP],
         "fa2_backward_host": [P] * 9 + [I] * 6 + [FP],
         "fa2_shard_range": [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)],
+        "fa2_tune_set": [ctypes.c_char_p, I],
         "fa2_last_error": [],
         "fa2_version": [],
         "fa2_device_count": [],
@@ -113,6 +114,29 @@ def version() -> int:
     return lib().fa2_version()
 
 
+def tune_set(knob, value: int = 0):
+    """Launch-plan override (tests and tools only; fa2_tune_set): ``tune_set(None)``
+    clears every override.  Nothing is read from the environment."""
+    _check(lib().fa2_tune_set(None if knob is None else knob.encode(), int(value)))
+
+
+class tuned:
+    """``with fa2amd.tuned(DKDV_QS=2, DKDV_WAVES=8): ...`` -- overrides for the block,
+    cleared on exit."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            tune_set(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        tune_set(None)
+        return False
+
+
 def shard_range(total_heads: int, shards: int, index: int):
     """Contiguous balanced head range of shard ``index`` (same rule as the C ABI)."""
     q, r = divmod(total_heads, shards)
@@ -123,18 +147,30 @@ def shard_range(total_heads: int, shards: int, index: int):
 # ---------------------------------------------------------------------------
 # device-tensor API (torch)
 # ---------------------------------------------------------------------------
-def _dev(t, name):
+def _dev(t, name, shape=None, device=None):
+    """Pointer of a contiguous fp32 GPU tensor, after checking its shape and that it
+    lives on `device` (the kernels read and write exactly B*H*S*D / B*H*S elements of
+    every pointer: a short or foreign tensor would be read out of bounds)."""
     import torch
 
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a torch.Tensor")
-    if not t.is_cuda:
-        raise FA2Error(f"{name} must be on a GPU (no CPU fallback in the product path)")
     if t.dtype != torch.float32:
         raise TypeError(f"{name} must be float32")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
+    if not t.is_cuda:
+        raise FA2Error(f"{name} must be on a GPU (no CPU fallback in the product path)")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
     return t.data_ptr()
+
+
+def _ptrs(named, B, H, S, D, device):
+    """[(tensor, name, kind)] -> pointers; kind 4 = [B,H,S,D], 3 = [B,H,S]."""
+    return [_dev(t, n, (B, H, S, D) if kind == 4 else (B, H, S), device) for t, n, kind in named]
 
 
 def _stream(stream, device):
@@ -159,12 +195,9 @@ def forward(q, k, v, precision="fp16", out=None, lse=None, stream=None):
     import torch
 
     B, H, S, D = _shape(q)
-    for t, n in ((k, "k"), (v, "v")):
-        if t.shape != q.shape:
-            raise ValueError(f"{n} shape {tuple(t.shape)} != q shape {tuple(q.shape)}")
     out = torch.empty_like(q) if out is None else out
     lse = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if lse is None else lse
-    ptrs = [_dev(t, n) for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out"), (lse, "lse"))]
+    ptrs = _ptrs(((q, "q", 4), (k, "k", 4), (v, "v", 4), (out, "out", 4), (lse, "lse", 3)), B, H, S, D, q.device)
     _check(lib().fa2_forward(*ptrs, B, H, S, D, _PRECISION[precision], _stream(stream, q.device)))
     return out, lse
 
@@ -174,7 +207,8 @@ def delta(dout, o, out=None, stream=None):
 
     B, H, S, D = _shape(o)
     out = torch.empty((B, H, S), device=o.device, dtype=torch.float32) if out is None else out
-    _check(lib().fa2_delta(_dev(dout, "dout"), _dev(o, "o"), _dev(out, "delta"), B, H, S, D, _stream(stream, o.device)))
+    ptrs = _ptrs(((dout, "dout", 4), (o, "o", 4), (out, "delta", 3)), B, H, S, D, o.device)
+    _check(lib().fa2_delta(*ptrs, B, H, S, D, _stream(stream, o.device)))
     return out
 
 
@@ -187,31 +221,31 @@ def backward(q, k, v, o, dout, lse, precision="fp16", dq=None, dk=None, dv=None,
     dk = torch.empty_like(q) if dk is None else dk
     dv = torch.empty_like(q) if dv is None else dv
     delta_buf = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if delta_buf is None else delta_buf
-    names = ("q", "k", "v", "o", "dout", "lse", "delta", "dq", "dk", "dv")
-    ptrs = [_dev(t, n) for t, n in zip((q, k, v, o, dout, lse, delta_buf, dq, dk, dv), names)]
+    ptrs = _ptrs(((q, "q", 4), (k, "k", 4), (v, "v", 4), (o, "o", 4), (dout, "dout", 4), (lse, "lse", 3),
+                  (delta_buf, "delta", 3), (dq, "dq", 4), (dk, "dk", 4), (dv, "dv", 4)), B, H, S, D, q.device)
     _check(lib().fa2_backward(*ptrs, B, H, S, D, _PRECISION[precision], _stream(stream, q.device)))
     return dq, dk, dv
 
 
 def backward_dkdv(q, k, v, dout, lse, delta_buf, dk, dv, stream=None):
     B, H, S, D = _shape(q)
-    ptrs = [_dev(t, n) for t, n in zip((q, k, v, dout, lse, delta_buf, dk, dv),
-                                       ("q", "k", "v", "dout", "lse", "delta", "dk", "dv"))]
+    ptrs = _ptrs(((q, "q", 4), (k, "k", 4), (v, "v", 4), (dout, "dout", 4), (lse, "lse", 3), (delta_buf, "delta", 3),
+                  (dk, "dk", 4), (dv, "dv", 4)), B, H, S, D, q.device)
     _check(lib().fa2_backward_dkdv(*ptrs, B, H, S, D, _stream(stream, q.device)))
 
 
 def backward_dq(q, k, v, dout, lse, delta_buf, dq, stream=None):
     B, H, S, D = _shape(q)
-    ptrs = [_dev(t, n) for t, n in zip((q, k, v, dout, lse, delta_buf, dq),
-                                       ("q", "k", "v", "dout", "lse", "delta", "dq"))]
+    ptrs = _ptrs(((q, "q", 4), (k, "k", 4), (v, "v", 4), (dout, "dout", 4), (lse, "lse", 3), (delta_buf, "delta", 3),
+                  (dq, "dq", 4)), B, H, S, D, q.device)
     _check(lib().fa2_backward_dq(*ptrs, B, H, S, D, _stream(stream, q.device)))
 
 
 def backward_dq_delta(q, k, v, o, dout, lse, delta_buf, dq, stream=None):
     """dQ with Δ = rowsum(dO * O) computed in the same kernel and written to delta_buf."""
     B, H, S, D = _shape(q)
-    ptrs = [_dev(t, n) for t, n in zip((q, k, v, o, dout, lse, delta_buf, dq),
-                                       ("q", "k", "v", "o", "dout", "lse", "delta", "dq"))]
+    ptrs = _ptrs(((q, "q", 4), (k, "k", 4), (v, "v", 4), (o, "o", 4), (dout, "dout", 4), (lse, "lse", 3),
+                  (delta_buf, "delta", 3), (dq, "dq", 4)), B, H, S, D, q.device)
     _check(lib().fa2_backward_dq_delta(*ptrs, B, H, S, D, _stream(stream, q.device)))
 
 
@@ -225,7 +259,8 @@ def naive_forward(q, k, v, out=None, lse=None, scores=None, stream=None):
     out = torch.empty_like(q) if out is None else out
     lse = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if lse is None else lse
     scores = torch.empty((B, H, S, S), device=q.device, dtype=torch.float32) if scores is None else scores
-    ptrs = [_dev(t, n) for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out"), (lse, "lse"), (scores, "scores"))]
+    ptrs = _ptrs(((q, "q", 4), (k, "k", 4), (v, "v", 4), (out, "out", 4), (lse, "lse", 3)), B, H, S, D, q.device)
+    ptrs.append(_dev(scores, "scores", (B, H, S, S), q.device))
     _check(lib().fa2_naive_forward(*ptrs, B, H, S, D, _stream(stream, q.device)))
     return out, lse, scores
 
@@ -239,7 +274,8 @@ def fa1_forward(q, k, v, out=None, l=None, m=None, stream=None):
     out = torch.empty_like(q) if out is None else out
     l = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if l is None else l
     m = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if m is None else m
-    ptrs = [_dev(t, n) for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out"), (l, "l"), (m, "m"))]
+    ptrs = _ptrs(((q, "q", 4), (k, "k", 4), (v, "v", 4), (out, "out", 4), (l, "l", 3), (m, "m", 3)), B, H, S, D,
+                 q.device)
     _check(lib().fa2_fa1_forward(*ptrs, B, H, S, D, _stream(stream, q.device)))
     return out, l, m
 
@@ -247,23 +283,35 @@ def fa1_forward(q, k, v, out=None, l=None, m=None, stream=None):
 # ---------------------------------------------------------------------------
 # host-array API (numpy): the reference host functions' semantics
 # ---------------------------------------------------------------------------
-def _np(a, name):
+def _np(a, name, shape=None):
+    """Pointer of a C-contiguous float32 array of exactly `shape` (the library copies
+    B*H*S*D / B*H*S floats from every host pointer)."""
     import numpy as np
 
     if not (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags.c_contiguous):
         raise TypeError(f"{name} must be a C-contiguous float32 numpy array")
+    if shape is not None and a.shape != tuple(shape):
+        raise ValueError(f"{name} has shape {a.shape}, expected {tuple(shape)}")
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _host_shape(q):
+    import numpy as np
+
+    if not isinstance(q, np.ndarray) or q.ndim != 4:
+        raise ValueError("expected q as a [B, H, S, D] numpy array")
+    return q.shape
 
 
 def forward_host(q, k, v, precision="fp32", num_devices=1):
     """(O, LSE, kernel_ms) from host arrays: host_flash_attention2_forward[_fp16] semantics."""
     import numpy as np
 
-    B, H, S, D = q.shape
+    B, H, S, D = _host_shape(q)
     o = np.empty_like(q)
     lse = np.empty((B, H, S), np.float32)
     ms = ctypes.c_float(0.0)
-    _check(lib().fa2_forward_host(_np(q, "q"), _np(k, "k"), _np(v, "v"), _np(o, "o"), _np(lse, "lse"),
+    _check(lib().fa2_forward_host(_np(q, "q"), _np(k, "k", q.shape), _np(v, "v", q.shape), _np(o, "o"), _np(lse, "lse"),
                                   B, H, S, D, _PRECISION[precision], num_devices, ctypes.byref(ms)))
     return o, lse, ms.value
 
@@ -272,10 +320,11 @@ def backward_host(q, k, v, o, dout, lse, precision="fp32", num_devices=1):
     """(dQ, dK, dV, kernel_ms) from host arrays: host_flash_attention2_backward[_fp16] semantics."""
     import numpy as np
 
-    B, H, S, D = q.shape
+    B, H, S, D = _host_shape(q)
     dq, dk, dv = np.empty_like(q), np.empty_like(q), np.empty_like(q)
     ms = ctypes.c_float(0.0)
-    _check(lib().fa2_backward_host(_np(q, "q"), _np(k, "k"), _np(v, "v"), _np(o, "o"), _np(dout, "dout"),
-                                   _np(lse, "lse"), _np(dq, "dq"), _np(dk, "dk"), _np(dv, "dv"),
+    _check(lib().fa2_backward_host(_np(q, "q"), _np(k, "k", q.shape), _np(v, "v", q.shape), _np(o, "o", q.shape),
+                                   _np(dout, "dout", q.shape), _np(lse, "lse", (B, H, S)), _np(dq, "dq"), _np(dk, "dk"),
+                                   _np(dv, "dv"),
                                    B, H, S, D, _PRECISION[precision], num_devices, ctypes.byref(ms)))
     return dq, dk, dv, ms.value

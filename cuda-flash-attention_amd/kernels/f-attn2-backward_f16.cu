@@ -26,10 +26,6 @@
 // Self-contained device code (hiprtc-compilable with -DCUPY_INLINE_COMPILE, C++14).
 #ifndef CUPY_INLINE_COMPILE
 #include "f-attn2.cuh"
-#ifdef FA2_STAMPS
-#include <cstdio>
-#include <vector>
-#endif
 #endif
 
 #ifdef FA2_TILE_BF16
@@ -78,16 +74,13 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 #endif
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// dS = P * (dP - Δ) for a pair of scores, as tile values.  FA2_DS_PK (fp16 tiles):
-// the product of the already-packed fp16 P and the packed (dP - Δ) (v_cvt_pk +
-// v_pk_mul_f16: one issue per score fewer than two f32 products and a conversion);
-// else the f32 products, rounded once.
-#ifndef FA2_DS_PK
-#define FA2_DS_PK 1
-#endif
+// dS = P * (dP - Δ) for a pair of scores, as tile values.  fp16 tiles: the product
+// of the already-packed fp16 P and the packed (dP - Δ) (v_cvt_pk + v_pk_mul_f16: one
+// issue per score fewer than two f32 products and a conversion); bf16 tiles: the f32
+// products, rounded once.
 typedef _Float16 tile2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ tile2 ds_pair(float p0, float p1, float d0, float d1, _Float16 ph0, _Float16 ph1) {
-#if FA2_DS_PK && !defined(FA2_TILE_BF16)
+#ifndef FA2_TILE_BF16
     (void)p0;
     (void)p1;
     return tile2{ph0, ph1} * tile2{(_Float16)d0, (_Float16)d1};
@@ -233,15 +226,12 @@ struct TileStager {
     }
 };
 
-// Row-coalesced prologue / epilogue (FA2_BWD_COAL).  A workgroup's stationary
+// Row-coalesced prologue / epilogue.  A workgroup's stationary
 // operand block (K and V for dK/dV, Q and dO for dQ) is one contiguous HBM range:
 // it is loaded whole rows at a time into the (still idle) LDS tile buffers as scaled
 // fp16 and read back as B fragments, instead of every lane fetching 16-B pieces of
 // its own row (32 rows per instruction).  Results leave through a wave-private LDS
 // stage as whole 128-B row segments.
-#ifndef FA2_BWD_COAL
-#define FA2_BWD_COAL 1
-#endif
 
 
 // Δ = rowsum(dO ∘ O) of a staged block's rows, from the row-coalesced registers of
@@ -302,9 +292,7 @@ struct DkdvState {
 // key on the lane (their accumulators start at -LSE*log2e and -Delta), P = exp2(S),
 // dS = P*(dP - Delta), then dV^T += dO^T P and dK^T += Q^T dS with P / dS packed as
 // B operands.  Every LDS fragment (Q / dO rows, dO^T / Q^T columns) feeds KB MFMAs.
-// ABL (timing ablations only, tools/kbench.py; results are wrong when set):
-//   2 = no softmax VALU, 8 = no dV/dK MFMAs, 16 = no S/dP MFMAs
-template <int D, int KB, int ABL = 0, typename Mid>
+template <int D, int KB, typename Mid>
 __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* Qs, const _Float16* dOs,
                                           const float* nlse2, const float* ndel, const FragOffsets<D>& fo, int h,
                                           Mid&& mid) {
@@ -329,15 +317,13 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
             sa[kb] = init_s;
             da[kb] = init_d;
         }
-        if (!(ABL & 16)) {
 #pragma unroll
-            for (int t = 0; t < D / 16; ++t) {
-                const f16x8 qa = fo.rowop(Qs, qb * 32, t), da_op = fo.rowop(dOs, qb * 32, t);
+        for (int t = 0; t < D / 16; ++t) {
+            const f16x8 qa = fo.rowop(Qs, qb * 32, t), da_op = fo.rowop(dOs, qb * 32, t);
 #pragma unroll
-                for (int kb = 0; kb < KB; ++kb) {
-                    sa[kb] = mfma(qa, st.kf[kb][t], sa[kb]);
-                    da[kb] = mfma(da_op, st.vf[kb][t], da[kb]);
-                }
+            for (int kb = 0; kb < KB; ++kb) {
+                sa[kb] = mfma(qa, st.kf[kb][t], sa[kb]);
+                da[kb] = mfma(da_op, st.vf[kb][t], da[kb]);
             }
         }
         f16x8 pf[KB][2], dsf[KB][2];
@@ -345,22 +331,10 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
         for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                if (ABL & 2) {
-                    pf[kb][i >> 3][i & 7] = to_tile(sa[kb][i]);
-                    dsf[kb][i >> 3][i & 7] = to_tile(da[kb][i]);
-                } else {
-                    const float p = fast_exp2(sa[kb][i]);
-                    pf[kb][i >> 3][i & 7] = to_tile(p);
-                    dsf[kb][i >> 3][i & 7] = to_tile(p * da[kb][i]);
-                }
+                const float p = fast_exp2(sa[kb][i]);
+                pf[kb][i >> 3][i & 7] = to_tile(p);
+                dsf[kb][i >> 3][i & 7] = to_tile(p * da[kb][i]);
             }
-        if (ABL & 8) {
-#pragma unroll
-            for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) asm volatile("" ::"v"(pf[kb][s]), "v"(dsf[kb][s]));
-            continue;
-        }
         // dV^T += dO^T P ; dK^T += Q^T dS over this query block's 32 rows
 #pragma unroll
         for (int b = 0; b < D / 32; ++b)
@@ -376,64 +350,16 @@ __device__ __forceinline__ void dkdv_step(DkdvState<D, KB>& st, const _Float16* 
     }
 }
 
-#ifndef FA2_DKDV_LP
-#define FA2_DKDV_LP 1
-#endif
-#ifndef FA2_DKDV_SW
+// Staging of the next Q/dO step in the dK/dV kernel is done by waves 0-3 only: stamps
+// showed waves 4-7 (which lose VALU arbitration to their SIMD partners) ~15 % slower
+// per step and the first half idling at the barrier (r01).  The dQ kernel's waves 4-7
+// run at s_setprio 1 (MI355X_MICROARCH §Two waves per SIMD, item 4: +1 %); its next-step
+// K/V loads are issued on the last step too (rows past S read as zeros through the
+// range-checked descriptor, no memory traffic), which removed 8 v_mov_b64 of
+// staging-register phi copies per step (+0.7 % at C3, +8.8 % at D = 128).
 #define FA2_DKDV_SW 4
-#endif
-// FA2_*_PRIO: s_setprio 1 for waves 4-7 of 8-wave workgroups (the second-dispatched
-// half loses VALU arbitration by age; MI355X_MICROARCH §Two waves per SIMD, item 4)
-// FA2_DKDV_QM_SW: staging waves of the QM > 1 instances (0 = all)
-#ifndef FA2_DKDV_QM_SW
-#define FA2_DKDV_QM_SW 0
-#endif
-#ifndef FA2_DKDV_PRIO
-#define FA2_DKDV_PRIO 0
-#endif
-#ifndef FA2_DQ_PRIO
-#define FA2_DQ_PRIO 1
-#endif
-#ifndef FA2_DQ_SW
-#define FA2_DQ_SW 0
-#endif
-// FA2_DQ_LOAD_ALWAYS: dQ issues the next step's K/V loads on the last step too (rows
-// past S read as zeros through the range-checked buffer descriptor, no memory traffic;
-// the LDS store stays guarded).  Conditional loads left the staging registers a phi of
-// old and new values, resolved with 8 v_mov_b64 per step on the common path.  dQ
-// +0.7 % at C3, +8.8 % at D = 128; the same in the forward and dK/dV measured -1 %
-// and -1.4 % (their loops have no such copies).
-#ifndef FA2_DQ_LOAD_ALWAYS
-#define FA2_DQ_LOAD_ALWAYS 1
-#endif
-#ifndef FA2_DQ_LP
-#define FA2_DQ_LP 1
-#endif
 
-// FA2_STAMPS (diagnostic builds only): s_memtime at the loop's segment boundaries,
-// per-wave sums written to `stamps` (read the shares, never the build's run time).
-#ifdef FA2_STAMPS
-#define FA2_NSTAMP 5
-#define FA2_STAMP(k)                                                                              \
-    do {                                                                                          \
-        __builtin_amdgcn_sched_barrier(0);                                                        \
-        unsigned long long t_;                                                                    \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
-        __builtin_amdgcn_sched_barrier(0);                                                        \
-        stv[k] += t_ - tprev;                                                                     \
-        tprev = t_;                                                                               \
-    } while (0)
-#define FA2_STAMP_ARG , unsigned long long* __restrict__ stamps
-#define FA2_STAMP_PASS , stamps
-#define FA2_STAMPS_ON 1
-#else
-#define FA2_STAMP(k)
-#define FA2_STAMP_ARG
-#define FA2_STAMP_PASS
-#define FA2_STAMPS_ON 0
-#endif
-
-// ---- dK, dV on v_mfma_f32_16x16x32 (FA2_TUNE_DKDV_MF=16) ------------------------
+// ---- dK, dV on v_mfma_f32_16x16x32 ----------------------------------------------
 // Same algorithm and data flow as dkdv_step; the wave's 32 keys are two 16-key
 // blocks nb.  Measured at the power cap on random data (tools/microbench/mfma_lds.hip):
 // 16x16x32 delivers 16 % more FLOPs per joule than 32x32x16 (it reads and writes a
@@ -487,7 +413,7 @@ struct FragOffsets16 {
     }
 };
 
-template <int D, int ABL = 0, typename Mid>
+template <int D, typename Mid>
 __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
                                             const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
                                             int g, Mid&& mid) {
@@ -505,19 +431,17 @@ __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* 
                 da[mb][nb] = dv;
             }
         }
-        if (!(ABL & 16)) {
 #pragma unroll
-            for (int ks = 0; ks < D / 32; ++ks)
+        for (int ks = 0; ks < D / 32; ++ks)
 #pragma unroll
-                for (int mb = 0; mb < 2; ++mb) {
-                    const f16x8 qa = fo.rowop(Qs, qb * 32 + 16 * mb, ks), doa = fo.rowop(dOs, qb * 32 + 16 * mb, ks);
+            for (int mb = 0; mb < 2; ++mb) {
+                const f16x8 qa = fo.rowop(Qs, qb * 32 + 16 * mb, ks), doa = fo.rowop(dOs, qb * 32 + 16 * mb, ks);
 #pragma unroll
-                    for (int nb = 0; nb < 2; ++nb) {
-                        sa[mb][nb] = mfma16(qa, st.kf[nb][ks], sa[mb][nb]);
-                        da[mb][nb] = mfma16(doa, st.vf[nb][ks], da[mb][nb]);
-                    }
+                for (int nb = 0; nb < 2; ++nb) {
+                    sa[mb][nb] = mfma16(qa, st.kf[nb][ks], sa[mb][nb]);
+                    da[mb][nb] = mfma16(doa, st.vf[nb][ks], da[mb][nb]);
                 }
-        }
+            }
         f16x8 pf[2], dsf[2];  // [nb], k-slot j <-> query 16 (j >> 2) + 4g + (j & 3)
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb)
@@ -525,25 +449,13 @@ __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* 
             for (int j = 0; j < 8; j += 2) {
                 const float sv0 = sa[j >> 2][nb][j & 3], dv0 = da[j >> 2][nb][j & 3];
                 const float sv1 = sa[j >> 2][nb][(j & 3) + 1], dv1 = da[j >> 2][nb][(j & 3) + 1];
-                if (ABL & 2) {
-                    pf[nb][j] = to_tile(sv0);
-                    pf[nb][j + 1] = to_tile(sv1);
-                    dsf[nb][j] = to_tile(dv0);
-                    dsf[nb][j + 1] = to_tile(dv1);
-                } else {
-                    const float p0 = fast_exp2(sv0), p1 = fast_exp2(sv1);
-                    pf[nb][j] = to_tile(p0);
-                    pf[nb][j + 1] = to_tile(p1);
-                    const tile2 d2 = ds_pair(p0, p1, dv0, dv1, pf[nb][j], pf[nb][j + 1]);
-                    dsf[nb][j] = d2[0];
-                    dsf[nb][j + 1] = d2[1];
-                }
+                const float p0 = fast_exp2(sv0), p1 = fast_exp2(sv1);
+                pf[nb][j] = to_tile(p0);
+                pf[nb][j + 1] = to_tile(p1);
+                const tile2 d2 = ds_pair(p0, p1, dv0, dv1, pf[nb][j], pf[nb][j + 1]);
+                dsf[nb][j] = d2[0];
+                dsf[nb][j + 1] = d2[1];
             }
-        if (ABL & 8) {
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) asm volatile("" ::"v"(pf[nb]), "v"(dsf[nb]));
-            continue;
-        }
 #pragma unroll
         for (int md = 0; md < D / 16; ++md) {
             const f16x8 a_do = fo.trop(dOs, qb * 32, md), a_q = fo.trop(Qs, qb * 32, md);
@@ -554,107 +466,6 @@ __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* 
             }
         }
     }
-}
-
-// FA2_DKDV_PIPE: the two 32-query blocks of a step software-pipelined inside the
-// wave (one basic block after mid()): S/dP MFMAs of block 1 are issued beside the
-// exp / dS VALU of block 0, and the dV/dK MFMAs of block 0 beside the VALU of block 1,
-// so each wave overlaps its own matrix and vector work instead of relying on its
-// SIMD partner only.  1 = source order only, 2 = plus sched_group_barrier interleave.
-#ifndef FA2_DKDV_PIPE
-#define FA2_DKDV_PIPE 0
-#endif
-
-template <int D>
-struct Dkdv16Blk {
-    f32x4 sa[2][2], da[2][2];  // [mb][nb]
-};
-
-template <int D>
-__device__ __forceinline__ void dkdv16_sdp(Dkdv16Blk<D>& b, const DkdvState16<D>& st, const _Float16* Qs,
-                                           const _Float16* dOs, const float* nlse2, const float* ndel,
-                                           const FragOffsets16<D>& fo, int g, int qb) {
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
-        const f32x4 lv = *reinterpret_cast<const f32x4*>(nlse2 + qb * 32 + 16 * mb + 4 * g);
-        const f32x4 dv = *reinterpret_cast<const f32x4*>(ndel + qb * 32 + 16 * mb + 4 * g);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            b.sa[mb][nb] = lv;
-            b.da[mb][nb] = dv;
-        }
-    }
-#pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks)
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            const f16x8 qa = fo.rowop(Qs, qb * 32 + 16 * mb, ks), doa = fo.rowop(dOs, qb * 32 + 16 * mb, ks);
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                b.sa[mb][nb] = mfma16(qa, st.kf[nb][ks], b.sa[mb][nb]);
-                b.da[mb][nb] = mfma16(doa, st.vf[nb][ks], b.da[mb][nb]);
-            }
-        }
-}
-
-template <int D>
-__device__ __forceinline__ void dkdv16_soft(const Dkdv16Blk<D>& b, f16x8 (&pf)[2], f16x8 (&dsf)[2]) {
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-            const float p0 = fast_exp2(b.sa[j >> 2][nb][j & 3]), p1 = fast_exp2(b.sa[j >> 2][nb][(j & 3) + 1]);
-            pf[nb][j] = to_tile(p0);
-            pf[nb][j + 1] = to_tile(p1);
-            const tile2 d2 = ds_pair(p0, p1, b.da[j >> 2][nb][j & 3], b.da[j >> 2][nb][(j & 3) + 1], pf[nb][j],
-                                     pf[nb][j + 1]);
-            dsf[nb][j] = d2[0];
-            dsf[nb][j + 1] = d2[1];
-        }
-}
-
-template <int D>
-__device__ __forceinline__ void dkdv16_acc(DkdvState16<D>& st, const f16x8 (&pf)[2], const f16x8 (&dsf)[2],
-                                           const _Float16* Qs, const _Float16* dOs, const FragOffsets16<D>& fo,
-                                           int qb) {
-#pragma unroll
-    for (int md = 0; md < D / 16; ++md) {
-        const f16x8 a_do = fo.trop(dOs, qb * 32, md), a_q = fo.trop(Qs, qb * 32, md);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            st.dva[md][nb] = mfma16(a_do, pf[nb], st.dva[md][nb]);
-            st.dka[md][nb] = mfma16(a_q, dsf[nb], st.dka[md][nb]);
-        }
-    }
-}
-
-// interleave the last `nm` MFMAs with `nv` VALU each (sched_group_barrier masks:
-// 0x8 MFMA, 0x2 VALU, 0x100 DS read)
-template <int NM, int NV>
-__device__ __forceinline__ void interleave_mfma_valu() {
-#pragma unroll
-    for (int i = 0; i < NM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
-    }
-}
-
-template <int D, typename Mid>
-__device__ __forceinline__ void dkdv_step16_pipe(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
-                                                 const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
-                                                 int g, Mid&& mid) {
-    Dkdv16Blk<D> b0, b1;
-    f16x8 pf0[2], dsf0[2], pf1[2], dsf1[2];
-    dkdv16_sdp<D>(b0, st, Qs, dOs, nlse2, ndel, fo, g, 0);
-    mid();
-    dkdv16_sdp<D>(b1, st, Qs, dOs, nlse2, ndel, fo, g, 1);
-    dkdv16_soft<D>(b0, pf0, dsf0);
-    if (FA2_DKDV_PIPE == 2) interleave_mfma_valu<D / 4, 3>();
-    dkdv16_acc<D>(st, pf0, dsf0, Qs, dOs, fo, 0);
-    dkdv16_soft<D>(b1, pf1, dsf1);
-    if (FA2_DKDV_PIPE == 2) interleave_mfma_valu<D / 4, 3>();
-    dkdv16_acc<D>(st, pf1, dsf1, Qs, dOs, fo, 1);
 }
 
 // a wave's 32 keys x D results (16x16 accumulator layout) through its LDS stage,
@@ -684,7 +495,6 @@ __device__ __forceinline__ void store_block_rows16(float (*os)[36], const f32x4 
 }
 
 // KB x 32 keys per wave, NW waves: grid BH * ceil(S / (32*KB*NK)), block 64*NW.
-// ABL: timing ablations (see dkdv_step; plus 1 = no staging in the loop, 4 = no barrier)
 // QS > 1 (small grids; 16x16x32 path): the query range is split over QS wave groups
 // of NK = NW / QS waves.  Wave w keeps keys of slot w % NK and takes query tiles
 // it·QS + w / NK; each step stages QS tiles.  After the loop the groups' dKᵀ / dVᵀ
@@ -692,9 +502,9 @@ __device__ __forceinline__ void store_block_rows16(float (*os)[36], const f32x4 
 // The workgroup's LDS: [buf][Q | dO][QS] fp16 tiles (or the query-split merge
 // records), [buf][-lse2 | -delta][QS] fp32 rows, the per-wave result stage.  Carved
 // from one block so the fused backward kernel can overlay it with the dQ role's.
-template <int D, int NW, int KB, int QS, int QM = 1>
+template <int D, int NW, int KB, int QS>
 struct DkdvLds {
-    static constexpr int QT = 64, TILE = QT * D, NK = NW / QS, TPS = QS * QM;
+    static constexpr int QT = 64, TILE = QT * D, NK = NW / QS;
     // query-split merge records: per wave of groups 1..QS-1, dKᵀ and dVᵀ (D floats per lane)
     static constexpr int MERGE = QS > 1 ? 2 * (QS - 1) * NK * D * 64 : 0;  // in halves
     // OVL: the prologue's K and V blocks side by side, loaded together with the first
@@ -702,41 +512,33 @@ struct DkdvLds {
     // unsplit C3 grid it measured -1.2 %)
     static constexpr bool OVL = QS > 1;
     static constexpr int KV = OVL ? 2 * 32 * KB * NK * D : 0;
-    static constexpr int SMEM0 = 2 * 2 * TPS * TILE > MERGE ? 2 * 2 * TPS * TILE : MERGE;
-    static constexpr int SMEM = (FA2_BWD_COAL && KV > SMEM0) ? KV : SMEM0;  // halves
-    static constexpr int ROWS = 2 * SMEM;                      // byte offsets
-    static constexpr int OSTAGE = ROWS + 2 * 2 * TPS * QT * 4;
-    static constexpr int BYTES = OSTAGE + (FA2_BWD_COAL ? NK * 32 * 36 * 4 : 0);
+    static constexpr int SMEM0 = 2 * 2 * QS * TILE > MERGE ? 2 * 2 * QS * TILE : MERGE;
+    static constexpr int SMEM = KV > SMEM0 ? KV : SMEM0;  // halves
+    static constexpr int ROWS = 2 * SMEM;                 // byte offsets
+    static constexpr int OSTAGE = ROWS + 2 * 2 * QS * QT * 4;
+    static constexpr int BYTES = OSTAGE + NK * 32 * 36 * 4;
 };
 
 // One workgroup of the dK/dV kernel; `bid` is its (XCD-remapped) block number over
-// the BH * ceil(S / (KPW * NK)) key blocks, `blk` the raw one (stamp records only).
-template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false, int QS = 1, int QM = 1>
-__device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int blk, const float* __restrict__ Q,
+// the BH * ceil(S / (KPW * NK)) key blocks.
+template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1>
+__device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const float* __restrict__ Q,
                                           const float* __restrict__ K, const float* __restrict__ V,
                                           const float* __restrict__ dO, const float* __restrict__ LSE,
                                           const float* __restrict__ Delta, float* __restrict__ dK,
-                                          float* __restrict__ dV, int S FA2_STAMP_ARG) {
-    using L = DkdvLds<D, NW, KB, QS, QM>;
-    // QM: query tiles per group per step (every wave of the group runs them one after
-    // the other: one barrier and one staging round per QM tiles).  The step's staged
-    // image holds TPS = QS * QM tiles; group g takes tiles g + QS * m.
-    constexpr int TPS = L::TPS;
-    static_assert(QM == 1 || (M16 && 2 * TPS <= NW && !FA2_STAMPS_ON), "QM > 1: 16x16x32, 2 TPS row waves");
+                                          float* __restrict__ dV, int S) {
+    using L = DkdvLds<D, NW, KB, QS>;
     constexpr int QT = L::QT;  // query rows per step
     constexpr int NT = 64 * NW;
     constexpr int TILE = L::TILE;
     constexpr int KPW = 32 * KB;  // keys per wave
-    static_assert(QS == 1 || (M16 && 2 * QS <= NW && !FA2_STAMPS_ON), "query split: 16x16x32, 2 QS row waves");
+    static_assert(QS == 1 || (M16 && 2 * QS <= NW), "query split: 16x16x32, 2 QS row waves");
     constexpr int NK = L::NK;  // key waves (QS > 1: waves w, w + NK, ... share keys)
     _Float16* smem = reinterpret_cast<_Float16*>(lds);
-    float(*rows)[2][TPS * QT] = reinterpret_cast<float(*)[2][TPS * QT]>(lds + L::ROWS);
-#if FA2_BWD_COAL
+    float(*rows)[2][QS * QT] = reinterpret_cast<float(*)[2][QS * QT]>(lds + L::ROWS);
     float(*ostage)[32][36] = reinterpret_cast<float(*)[32][36]>(lds + L::OSTAGE);  // per-wave result stage
-#endif
-    (void)blk;
 
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
     const int wave = QS > 1 ? (tid >> 6) % NK : tid >> 6;  // key slot of the wave
     const int qg = QS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NK) : 0;  // query group
     const int nkb = (S + KPW * NK - 1) / (KPW * NK);
@@ -750,13 +552,11 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
     FragOffsets<D> fo;
     fo.init(lane);
     // 16x16x32 path (M16): its own state / offsets; the unused set is dead code
-    static_assert(!M16 || (KB == 1 && FA2_BWD_COAL), "16x16x32 dK/dV: 32 keys per wave, coalesced prologue");
+    static_assert(!M16 || KB == 1, "16x16x32 dK/dV: 32 keys per wave");
     DkdvState16<D> st16;
     FragOffsets16<D> fo16;
     const int g16 = lane >> 4;
     if constexpr (M16) fo16.init(lane);
-    (void)r;
-#if FA2_BWD_COAL
     // Prologue.  L::OVL: the K and V blocks and the first Q/dO step are loaded in one
     // go (one HBM round trip instead of three), K and V side by side in the LDS block;
     // else K, then V, each through the Q/dO buffers.
@@ -806,7 +606,6 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
         read_v();
         __syncthreads();
     }
-#endif
     if constexpr (M16) {
 #pragma unroll
         for (int md = 0; md < D / 16; ++md)
@@ -815,36 +614,24 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
                 st16.dka[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
                 st16.dva[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-    }
+    } else {
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-#if !FA2_BWD_COAL
-        const int key = key0 + kb * 32 + r;
+        for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int t = 0; t < D / 16; ++t) {
-            st.kf[kb][t] = load_frag(K + base + (long)key * D + 16 * t + 8 * h, key < S, kscale);
-            st.vf[kb][t] = load_frag(V + base + (long)key * D + 16 * t + 8 * h, key < S, 1.f);
-        }
-#endif
+            for (int b = 0; b < D / 32; ++b)
 #pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                st.dka[kb][b][i] = 0.f;
-                st.dva[kb][b][i] = 0.f;
-            }
+                for (int i = 0; i < 16; ++i) {
+                    st.dka[kb][b][i] = 0.f;
+                    st.dva[kb][b][i] = 0.f;
+                }
     }
 
-    // Staging of the next Q/dO step is done by the first FA2_DKDV_SW waves only (all
-    // NW when 0): stamps showed waves NW/2..NW-1 (which lose VALU arbitration to their
-    // SIMD partners) ~15 % slower per step and the first half idling at the barrier,
-    // so the staging work goes to the first half.
-    constexpr int SW = QM > 1 ? (FA2_DKDV_QM_SW > 0 && FA2_DKDV_QM_SW < NW ? FA2_DKDV_QM_SW : NW)
-                              : (FA2_DKDV_SW > 0 && FA2_DKDV_SW < NW) ? FA2_DKDV_SW : NW;
+    // next-step staging by the first SW waves (FA2_DKDV_SW, above)
+    constexpr int SW = FA2_DKDV_SW < NW ? FA2_DKDV_SW : NW;
     constexpr int NS = 64 * SW;
     const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool stg = wave_u < SW;
-    TileStager<D, QT * TPS, NS> qs, dos;
+    TileStager<D, QT * QS, NS> qs, dos;
     qs.init(Q + base, S, tid);
     dos.init(dO + base, S, tid);
     // Row constants of the staged step: wave 0 carries LSE, wave 1 carries Delta
@@ -855,40 +642,30 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
     // (QS > 1: waves 0..QS-1 carry the LSE rows of the step's QS tiles, waves
     // QS..2QS-1 the Delta rows)
     static_assert(QT == 64, "one wave per row vector");
-    if (FA2_DKDV_PRIO && NW == 8 && wave_u >= NW / 2) __builtin_amdgcn_s_setprio(1);
     const __amdgpu_buffer_rsrc_t rs_lse = head_rsrc(LSE + rbase, S, 1);
     const __amdgpu_buffer_rsrc_t rs_del = head_rsrc(Delta + rbase, S, 1);
     float rowraw = 0.f;
     int rowq = 0;
-    const int rw = wave_u % TPS;  // which of the step's tiles this wave's row vector is
+    const int rw = wave_u % QS;  // which of the step's tiles this wave's row vector is
     auto load_rows = [&](int q0) {
         q0 += rw * QT;
         rowq = q0 + lane;
-        if (wave_u < TPS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
-        else if (wave_u < 2 * TPS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_del, lane * 4, q0 * 4, 0));
+        if (wave_u < QS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
+        else if (wave_u < 2 * QS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_del, lane * 4, q0 * 4, 0));
     };
     auto store_rows = [&](int buf) {
         // stored negated: they are the initial accumulators of S and dP
-        if (wave_u < TPS) rows[buf][0][rw * QT + lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
-        else if (wave_u < 2 * TPS) rows[buf][1][rw * QT + lane] = -rowraw;
+        if (wave_u < QS) rows[buf][0][rw * QT + lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
+        else if (wave_u < 2 * QS) rows[buf][1][rw * QT + lane] = -rowraw;
     };
-    // where the next step's global loads are issued (all eight waves issuing them at
-    // once right after the barrier queue on the texture unit): FA2_DKDV_LP
-    // 0 = all at the step start, 1 = all between the two query blocks, 2 = Q at the
-    // start and dO + row constants between the blocks
-    auto load_a = [&](int it) {
-        if ((FA2_DKDV_LP == 0 || FA2_DKDV_LP == 2) && stg) qs.load(it * TPS * QT);
-        if (FA2_DKDV_LP == 0) {
-            if (stg) dos.load(it * TPS * QT);
-            load_rows(it * TPS * QT);
+    // the next step's global loads go out between the step's two query blocks (issued
+    // all at once right after the barrier they queue on the texture unit: r01)
+    auto load_next = [&](int it) {
+        if (stg) {
+            qs.load(it * QS * QT);
+            dos.load(it * QS * QT);
         }
-    };
-    auto load_b = [&](int it) {
-        if (FA2_DKDV_LP == 1 && stg) qs.load(it * TPS * QT);
-        if (FA2_DKDV_LP != 0) {
-            if (stg) dos.load(it * TPS * QT);
-            load_rows(it * TPS * QT);
-        }
+        load_rows(it * QS * QT);
     };
     auto store_step = [&](_Float16* qdst, _Float16* ddst, int rbuf) {
         if (stg) {
@@ -898,13 +675,12 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
         store_rows(rbuf);
     };
     const int nqt = (S + QT - 1) / QT;  // query tiles
-    const int nsteps = (nqt + TPS - 1) / TPS;
+    const int nsteps = (nqt + QS - 1) / QS;
     if (stg) {
         qs.load(0);
         dos.load(0);
     }
     load_rows(0);
-#if FA2_BWD_COAL
     if constexpr (L::OVL) {
         kst.store(smem, kscale, tid);
         vst.store(vblk, 1.f, tid);
@@ -913,72 +689,41 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
         read_v();
         __syncthreads();
     }
-#endif
-    store_step(smem, smem + TPS * TILE, 0);
+    store_step(smem, smem + QS * TILE, 0);
     __syncthreads();
     // the group's tile within each staged image: folded into the per-lane offsets
     if (QS > 1) fo16.shift(qg * TILE);
     const int rq = qg * QT;  // the group's row constants
 
-#ifdef FA2_STAMPS
-    unsigned long long stv[FA2_NSTAMP] = {0, 0, 0, 0, 0}, tprev;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
-#endif
-    // one staged step: the group's QM tiles g + QS m, each one dkdv_step16 (the next
-    // step's mid-step loads inside the first)
+    // one staged step: the group's tile (the next step's loads inside it)
     auto run_step = [&](const _Float16* Qb, const _Float16* dOb, const float* r0, const float* r1, int itc,
                         auto&& mid) {
         if constexpr (M16) {
-#pragma unroll
-            for (int m = 0; m < QM; ++m) {
-                const bool live = (QS == 1 && QM == 1) || itc * TPS + qg + QS * m < nqt;  // wave-uniform
-                if (!live) {
-                    if (m == 0) mid();
-                } else if (m == 0) {
-                    if (FA2_DKDV_PIPE && ABL == 0)
-                        dkdv_step16_pipe<D>(st16, Qb, dOb, r0 + rq, r1 + rq, fo16, g16, mid);
-                    else dkdv_step16<D, ABL>(st16, Qb, dOb, r0 + rq, r1 + rq, fo16, g16, mid);
-                } else {
-                    dkdv_step16<D, ABL>(st16, Qb + m * QS * TILE, dOb + m * QS * TILE, r0 + rq + m * QS * QT,
-                                        r1 + rq + m * QS * QT, fo16, g16, [] {});
-                }
-            }
+            const bool live = QS == 1 || itc * QS + qg < nqt;  // wave-uniform
+            if (!live) mid();
+            else dkdv_step16<D>(st16, Qb, dOb, r0 + rq, r1 + rq, fo16, g16, mid);
         } else {
-            dkdv_step<D, KB, ABL>(st, Qb, dOb, r0, r1, fo, h, mid);
+            dkdv_step<D, KB>(st, Qb, dOb, r0, r1, fo, h, mid);
         }
     };
     for (int it = 0; it < nsteps; it += 2) {
         {
-            const bool more = !(ABL & 1) && it + 1 < nsteps;
-            if (more) load_a(it + 1);
-            FA2_STAMP(0);
-            run_step(smem, smem + TPS * TILE, rows[0][0], rows[0][1], it, [&] {
-                if (more) load_b(it + 1);
+            const bool more = it + 1 < nsteps;
+            run_step(smem, smem + QS * TILE, rows[0][0], rows[0][1], it, [&] {
+                if (more) load_next(it + 1);
             });
-            FA2_STAMP(1);
-            if (more) store_step(smem + 2 * TPS * TILE, smem + 3 * TPS * TILE, 1);
-            FA2_STAMP(2);
-            if (!(ABL & 4)) __syncthreads();
-            FA2_STAMP(3);
+            if (more) store_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, 1);
+            __syncthreads();
         }
         if (it + 1 < nsteps) {
-            const bool more = !(ABL & 1) && it + 2 < nsteps;
-            if (more) load_a(it + 2);
-            FA2_STAMP(0);
-            run_step(smem + 2 * TPS * TILE, smem + 3 * TPS * TILE, rows[1][0], rows[1][1], it + 1, [&] {
-                if (more) load_b(it + 2);
+            const bool more = it + 2 < nsteps;
+            run_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0], rows[1][1], it + 1, [&] {
+                if (more) load_next(it + 2);
             });
-            FA2_STAMP(1);
-            if (more) store_step(smem, smem + TPS * TILE, 0);
-            FA2_STAMP(2);
-            if (!(ABL & 4)) __syncthreads();
-            FA2_STAMP(3);
+            if (more) store_step(smem, smem + QS * TILE, 0);
+            __syncthreads();
         }
     }
-#ifdef FA2_STAMPS
-    if (lane == 0)
-        for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blk * NW + wave) * FA2_NSTAMP + k] = stv[k];
-#endif
 
     if constexpr (QS > 1) {
         // query-split merge (the loop ended on a barrier: the tile buffers are free);
@@ -1013,50 +758,26 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, int b
         }
     }
     const float dscale = 1.f / __builtin_sqrtf((float)D);
-#if FA2_BWD_COAL
     if constexpr (M16) {
         store_block_rows16<D>(ostage[wave], st16.dka, dscale, dK + base + (long)key0 * D, S - key0, lane);
         store_block_rows16<D>(ostage[wave], st16.dva, 1.f, dV + base + (long)key0 * D, S - key0, lane);
-        return;
-    }
+    } else {
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-        const int k0r = key0 + kb * 32;
-        store_block_rows<D>(ostage[wave], st.dka[kb], dscale, dK + base + (long)k0r * D, S - k0r, lane);
-        store_block_rows<D>(ostage[wave], st.dva[kb], 1.f, dV + base + (long)k0r * D, S - k0r, lane);
-    }
-#else
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-        const int key = key0 + kb * 32 + r;
-        if (key < S) {
-            float* dkrow = dK + base + (long)key * D;
-            float* dvrow = dV + base + (long)key * D;
-#pragma unroll
-            for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const f32x16& ka = st.dka[kb][b];
-                    const f32x16& va = st.dva[kb][b];
-                    f32x4 a = {ka[4 * g] * dscale, ka[4 * g + 1] * dscale, ka[4 * g + 2] * dscale, ka[4 * g + 3] * dscale};
-                    f32x4 c = {va[4 * g], va[4 * g + 1], va[4 * g + 2], va[4 * g + 3]};
-                    *reinterpret_cast<f32x4*>(dkrow + 32 * b + 8 * g + 4 * h) = a;
-                    *reinterpret_cast<f32x4*>(dvrow + 32 * b + 8 * g + 4 * h) = c;
-                }
+        for (int kb = 0; kb < KB; ++kb) {
+            const int k0r = key0 + kb * 32;
+            store_block_rows<D>(ostage[wave], st.dka[kb], dscale, dK + base + (long)k0r * D, S - k0r, lane);
+            store_block_rows<D>(ostage[wave], st.dva[kb], 1.f, dV + base + (long)k0r * D, S - k0r, lane);
         }
     }
-#endif
 }
 
-template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false, int QS = 1, int QM = 1>
+template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                         const float* __restrict__ dO, const float* __restrict__ LSE,
-                        const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV,
-                        int S FA2_STAMP_ARG) {
-    __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, KB, QS, QM>::BYTES];
-    dkdv_body<D, NW, KB, ABL, M16, QS, QM>(lds, xcd_remap(blockIdx.x, gridDim.x), blockIdx.x, Q, K, V, dO, LSE, Delta, dK,
-                                       dV, S FA2_STAMP_PASS);
+                        const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV, int S) {
+    __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, KB, QS>::BYTES];
+    dkdv_body<D, NW, KB, M16, QS>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE, Delta, dK, dV, S);
 }
 
 // ---------------------------------------------------------------------------
@@ -1077,7 +798,7 @@ __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, cons
     f16x8 dsf[NKB][2];
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
-        if (NKB > 1 && kb == 1) mid();  // between the two key blocks (next tile's loads, FA2_DQ_LP)
+        if (NKB > 1 && kb == 1) mid();  // between the two key blocks (the next tile's loads)
         // rows: key k0 + kb*32 + (i&3) + 8*(i>>2) + 4h ; col: query (lane)
         f32x16 sa = st.nlse2, da = st.ndel;
 #pragma unroll
@@ -1102,7 +823,7 @@ __device__ __forceinline__ void dq_tile(DqState<D>& st, const _Float16* Ks, cons
             for (int s = 0; s < 2; ++s) st.dqa[b] = mfma(fo.trop(Ks, kb * 32 + 16 * s, b), dsf[kb][s], st.dqa[b]);
 }
 
-// ---- dQ on v_mfma_f32_16x16x32 (FA2_TUNE_DQ_MF=16), maps as in dkdv_step16:
+// ---- dQ on v_mfma_f32_16x16x32, maps as in dkdv_step16:
 //   S^T / dP^T (m = key, n = query, k = d): A = K / V rows of the tile (row reads),
 //     B = Q / dO fragments in VGPRs; accumulators start at the lane's -lse2 / -delta.
 //   dQ^T (m = d, n = query, k = key): B = dS^T packed k-slot j <-> key
@@ -1120,7 +841,7 @@ __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, 
     f16x8 dsf[NKB][2];  // [32-key half kb][nb]
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
-        if (NKB > 1 && kb == 1) mid();  // the next tile's loads between the two 32-key halves (FA2_DQ_LP)
+        if (NKB > 1 && kb == 1) mid();  // the next tile's loads between the two 32-key halves
         f32x4 sa[2][2], da[2][2];  // [mbl][nb]: keys k0 + 32 kb + 16 mbl + 4g + i
 #pragma unroll
         for (int mbl = 0; mbl < 2; ++mbl)
@@ -1188,7 +909,7 @@ struct DqLds {
     static constexpr int SMEM0 = 4 * KS * TILE > QD ? 4 * KS * TILE : QD;
     static constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;  // halves
     static constexpr int OSTAGE = 2 * SMEM;                     // byte offsets
-    static constexpr int DBLK = OSTAGE + (FA2_BWD_COAL ? NQ * 32 * 36 * 4 : 0);
+    static constexpr int DBLK = OSTAGE + NQ * 32 * 36 * 4;
     static constexpr int BYTES = DBLK + (DELTA ? 32 * NQ : 1) * 4;
 };
 
@@ -1207,9 +928,7 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     static_assert(KS == 1 || (M16 && NW % KS == 0), "key split: 16x16x32");
     constexpr int NQ = L::NQ;  // query waves (KS > 1: waves w, w + NQ, ... share rows)
     _Float16* smem = reinterpret_cast<_Float16*>(lds);
-#if FA2_BWD_COAL
     float(*ostage)[32][36] = reinterpret_cast<float(*)[32][36]>(lds + L::OSTAGE);  // per-wave dQ stage
-#endif
     float* delta_blk = reinterpret_cast<float*>(lds + L::DBLK);
 
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -1225,13 +944,11 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     DqState<D> st;
     FragOffsets<D> fo;
     fo.init(lane);
-    static_assert(!M16 || FA2_BWD_COAL, "16x16x32 dQ: coalesced prologue");
     DqState16<D> st16;
     FragOffsets16<D> fo16;
     const int g16 = lane >> 4, i16 = lane & 15;
     if constexpr (M16) fo16.init(lane);
-    // K/V staging by the first FA2_DQ_SW waves (all when 0), as in the dK/dV kernel
-    constexpr int SW = (FA2_DQ_SW > 0 && FA2_DQ_SW < NW) ? FA2_DQ_SW : NW;
+    constexpr int SW = NW;  // K/V staging by every wave (by waves 0-3 only: no gain, r01)
     TileStager<D, KT * KS, 64 * SW> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
@@ -1243,7 +960,6 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     const int ntiles = (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     const int nsteps = (ntiles + KS - 1) / KS;
-#if FA2_BWD_COAL
     // Prologue.  L::OVL: the Q and dO blocks (and O for Δ) and the first K/V step are
     // loaded in one go (one HBM round trip instead of three), Q and dO in the second
     // K/V buffer, which the first loop step restages only after the barrier below;
@@ -1306,20 +1022,9 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
         read_d();
         if constexpr (!OVL) __syncthreads();
     }
-#else
-#pragma unroll
-    for (int t = 0; t < D / 16; ++t) {
-        st.qf[t] = load_frag(Q + base + (long)q * D + 16 * t + 8 * h, qvalid, qscale);
-        st.df[t] = load_frag(dO + base + (long)q * D + 16 * t + 8 * h, qvalid, 1.f);
-    }
-#endif
     {
         const float nl = qvalid ? -LSE[(long)bh * S + q] * FA2B_LOG2E : -__builtin_inff();
-#if FA2_BWD_COAL
         const float nd = !qvalid ? 0.f : DELTA ? -delta_blk[wave * 32 + r] : -Delta[(long)bh * S + q];
-#else
-        const float nd = qvalid ? -Delta[(long)bh * S + q] : 0.f;
-#endif
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             st.nlse2[i] = nl;
@@ -1345,8 +1050,8 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) st16.dqa[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    if (FA2_DQ_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(tid >> 6) >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    if (!FA2_BWD_COAL || !L::OVL) {
+    if (NW == 8 && __builtin_amdgcn_readfirstlane(tid >> 6) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    if (!L::OVL) {
         ks.load(0);
         vs.load(0);
         ks.store(smem, 1.f, tid);
@@ -1365,10 +1070,7 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
                 ks.load((j + 1) * KS * KT);
                 vs.load((j + 1) * KS * KT);
             };
-            if ((FA2_DQ_LOAD_ALWAYS || more) && !FA2_DQ_LP) ld();
-            auto mid = [&] {
-                if ((FA2_DQ_LOAD_ALWAYS || more) && FA2_DQ_LP) ld();
-            };
+            auto mid = [&] { ld(); };  // also on the last step (see FA2_DKDV_SW's note)
             if constexpr (M16) {
                 if (!live) mid();
                 else if (jj == last_ragged) dq_tile16<D, true, NKB>(st16, smem, smem + KS * TILE, fo16, jj * KT, S, g16, mid);
@@ -1391,10 +1093,7 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
                 ks.load((j + 2) * KS * KT);
                 vs.load((j + 2) * KS * KT);
             };
-            if ((FA2_DQ_LOAD_ALWAYS || more) && !FA2_DQ_LP) ld();
-            auto mid = [&] {
-                if ((FA2_DQ_LOAD_ALWAYS || more) && FA2_DQ_LP) ld();
-            };
+            auto mid = [&] { ld(); };  // also on the last step (see FA2_DKDV_SW's note)
             if constexpr (M16) {
                 if (!live) mid();
                 else if (jj == last_ragged)
@@ -1440,7 +1139,6 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
                     for (int i = 0; i < 4; ++i) st16.dqa[md][nb][i] += rec[((md * 2 + nb) * 4 + i) * 64 + lane];
         }
     }
-#if FA2_BWD_COAL
     {
         const int q0w = qb * 32 * NQ + wave * 32;
         if constexpr (M16)
@@ -1450,20 +1148,6 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
             store_block_rows<D>(ostage[wave], st.dqa, 1.f / __builtin_sqrtf((float)D), dQ + base + (long)q0w * D,
                                 S - q0w, lane);
     }
-#else
-    if (qvalid) {
-        const float dscale = 1.f / __builtin_sqrtf((float)D);
-        float* row = dQ + base + (long)q * D;
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                f32x4 a = {st.dqa[b][4 * g] * dscale, st.dqa[b][4 * g + 1] * dscale, st.dqa[b][4 * g + 2] * dscale,
-                           st.dqa[b][4 * g + 3] * dscale};
-                *reinterpret_cast<f32x4*>(row + 32 * b + 8 * g + 4 * h) = a;
-            }
-    }
-#endif
 }
 
 template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1>
@@ -1475,7 +1159,6 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
     dq_body<D, NW, DELTA, NKB, M16, KS>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE, Delta, dQ, S, O);
 }
 
-#ifndef FA2_STAMPS
 // dK/dV and dQ in ONE launch (small grids).  Workgroups [0, ndk) take the dK/dV role
 // (QS query groups), [ndk, gridDim.x) the dQ role (KS key groups); the two roles
 // share nothing, so they run side by side on the chip instead of one kernel after
@@ -1492,12 +1175,11 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
     __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
     const int b = blockIdx.x;
     if (b < ndk)
-        dkdv_body<D, NW, 1, 0, true, QS>(lds, xcd_remap(b, ndk), b, Q, K, V, dO, LSE, Delta, dK, dV, S);
+        dkdv_body<D, NW, 1, true, QS>(lds, xcd_remap(b, ndk), Q, K, V, dO, LSE, Delta, dK, dV, S);
     else
         dq_body<D, NW, false, NKB, true, KS>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
                                              const_cast<float*>(Delta), dQ, S, nullptr);
 }
-#endif
 
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
 // block 256, test_flash_attention2.py:499-535 / f-attn2-backward_f16.cu:445),
@@ -1684,93 +1366,32 @@ __device__ __forceinline__ void delta_row_body(const float* __restrict__ dO, con
 namespace fa2 {
 
 namespace {
-#ifdef FA2_STAMPS
-struct StampLog {
-    double sum[FA2_NSTAMP] = {};
-    long launches = 0;
-    ~StampLog() {
-        double t = 0;
-        for (double x : sum) t += x;
-        if (!launches || t <= 0) return;
-        const char* names[FA2_NSTAMP] = {"load-issue", "step", "lds-store", "barrier", "-"};
-        fprintf(stderr, "[fa2 stamps] dkdv launches=%ld cycles/wave/launch=%.0f\n", launches, t / launches);
-        for (int k = 0; k < 4; ++k) fprintf(stderr, "[fa2 stamps]   %-12s %5.1f %%\n", names[k], 100 * sum[k] / t);
-    }
-};
-StampLog g_dkdv_stamps;
-#endif
-// waves per workgroup: 8 x 32 keys for D <= 64 (2 waves/SIMD fit in 256 VGPRs);
-// D = 128 needs more than 256 registers per lane, so 4 waves (1 per SIMD).
-// query-split instances (QS > 1: NW / QS key waves per workgroup, 16x16x32, no stamps)
-template <int D, int NW, int QS>
-hipError_t dkdv_launch_qs(const float* q, const float* k, const float* v, const float* dout, const float* lse,
-                          const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-#ifdef FA2_STAMPS
-    return hipErrorNotSupported;
-#else
-    const long grid = (long)bh * ((S + 32 * (NW / QS) - 1) / (32 * (NW / QS)));
-    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, 1, 0, true, QS>), dim3((unsigned)grid), dim3(64 * NW),
-                       0, stream, q, k, v, dout, lse, delta, dk, dv, S);
-    return hipGetLastError();
-#endif
-}
-
-template <int D, int NW, int QM>
-hipError_t dkdv_launch_qm(const float* q, const float* k, const float* v, const float* dout, const float* lse,
-                          const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-#ifdef FA2_STAMPS
-    return hipErrorNotSupported;
-#else
-    const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
-    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, 1, 0, true, 1, QM>), dim3((unsigned)grid),
-                       dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dk, dv, S);
-    return hipGetLastError();
-#endif
-}
-
-template <int D, int NW, int KB = 1, int ABL = 0, bool M16 = false>
+// dK/dV kernel instances (NW waves x 32 keys; QS query groups).  16x16x32 everywhere
+// but the 2-wave instance: at the power cap on random data 16x16x32 delivers 16 %
+// more FLOPs per joule than 32x32x16 (+5 % at C3, +4 % at D = 128, +7 % on small
+// D = 64 grids); the 2-wave instance keeps 32x32x16.
+template <int D, int NW, bool M16 = true, int QS = 1>
 hipError_t dkdv_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                        const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-    const long grid = (long)bh * ((S + 32 * KB * NW - 1) / (32 * KB * NW));
+    const long grid = (long)bh * ((S + 32 * (NW / QS) - 1) / (32 * (NW / QS)));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-#ifdef FA2_STAMPS
-    static unsigned long long* buf = nullptr;
-    static long cap = 0;
-    const long n = grid * NW * FA2_NSTAMP;
-    if (n > cap) {
-        if (buf) (void)hipFree(buf);
-        (void)hipMalloc(&buf, n * sizeof(unsigned long long));
-        cap = n;
-    }
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, KB, ABL, M16>), dim3((unsigned)grid), dim3(64 * NW),
-                       0, stream, q, k, v, dout, lse, delta, dk, dv, S, buf);
-    std::vector<unsigned long long> hst(n);
-    (void)hipStreamSynchronize(stream);
-    (void)hipMemcpy(hst.data(), buf, n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-    for (long i = 0; i < n; ++i) g_dkdv_stamps.sum[i % FA2_NSTAMP] += (double)hst[i] / (grid * NW);
-    ++g_dkdv_stamps.launches;
-#else
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, KB, ABL, M16>), dim3((unsigned)grid), dim3(64 * NW),
-                       0, stream, q, k, v, dout, lse, delta, dk, dv, S);
-#endif
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_kernel<D, NW, 1, M16, QS>), dim3((unsigned)grid), dim3(64 * NW), 0,
+                       stream, q, k, v, dout, lse, delta, dk, dv, S);
     return hipGetLastError();
 }
-// Geometry (FA2_TUNE_DKDV_WAVES / FA2_TUNE_DKDV_KB): 8 waves x 32 keys for D <= 64
-// (2 waves/SIMD in 256 VGPRs), or 4 waves x 64 keys (1 wave/SIMD, 512 registers,
-// every LDS fragment feeding two MFMAs); D = 128 always 4 x 32.
+// Geometry: 8 waves x 32 keys for D <= 64 (2 waves/SIMD in 256 VGPRs); D = 128 4 x 32
+// (more than 256 registers per lane); fewer waves where the grid would leave CUs idle.
+// Launch-plan overrides (fa2_tune_set, tests and tools only): DKDV_WAVES, DKDV_QS.
 template <int D>
 hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                          const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-    // FA2_TUNE_DKDV_WAVES = 0 (default): auto_waves over the grid of 32-key wave units
-    int nw = tune_knob("DKDV_WAVES", 0);
+    int nw = tune_knob("DKDV_WAVES", 0);  // 0 = auto_waves over the grid of 32-key wave units
     const long units = (long)bh * ((S + 31) / 32);
-    // FA2_TUNE_DKDV_QS: query groups per workgroup (0 = auto).  Auto, where 8-wave
-    // workgroups of one key block per wave would leave CUs idle: below 8 key blocks
-    // per CU QS = 2 at 8 waves; below 4, D = 32 QS = 4 at 8 waves and D = 64 QS = 2 at
-    // 4 waves (at QS = 4 its 4-tile staging registers spill).  Measured (B2_H8_D64,
-    // r01): S = 512 16.1 -> 12.1 us, 1024 29.1 -> 20.8, 2048 53.7 -> 44.3.
+    // Query groups per workgroup (0 = auto).  Auto, where 8-wave workgroups of one key
+    // block per wave would leave CUs idle: below 8 key blocks per CU QS = 2 at 8 waves;
+    // below 4, D = 32 QS = 4 at 8 waves and D = 64 QS = 2 at 4 waves (at QS = 4 its
+    // 4-tile staging registers spill).  Measured (B2_H8_D64, r01): S = 512 16.1 -> 12.1
+    // us, 1024 29.1 -> 20.8, 2048 53.7 -> 44.3.
     int qs = tune_knob("DKDV_QS", 0);
     if (qs == 0 && nw == 0 && D <= 64) {
         const int a = auto_waves(units, 8);
@@ -1780,44 +1401,14 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     }
     if (nw == 0) nw = auto_waves(units, D <= 64 ? 8 : 4);
     if constexpr (D <= 64) {
-        if (qs == 2 && nw == 8) return dkdv_launch_qs<D, 8, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-        if (qs == 2 && nw == 4) return dkdv_launch_qs<D, 4, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        if (qs == 2 && nw == 8) return dkdv_launch<D, 8, true, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        if (qs == 2 && nw == 4) return dkdv_launch<D, 4, true, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        if (nw == 8) return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     }
     if constexpr (D <= 32) {
-        if (qs == 4 && nw == 8) return dkdv_launch_qs<D, 8, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+        if (qs == 4 && nw == 8) return dkdv_launch<D, 8, true, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     }
-    const int kbk = tune_knob("DKDV_KB", 1);
-#ifdef FA2_ABLATIONS
-    if constexpr (D == 64) {
-        if (nw == 8) switch (tune_knob("DKDV_ABL", 0)) {
-            case 1: return dkdv_launch<D, 8, 1, 1>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-            case 2: return dkdv_launch<D, 8, 1, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-            case 4: return dkdv_launch<D, 8, 1, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-            case 8: return dkdv_launch<D, 8, 1, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-            case 16: return dkdv_launch<D, 8, 1, 16>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-            default: break;
-        }
-    }
-#endif
-    if constexpr (D <= 64) {
-        if (kbk == 2) {
-            return dkdv_launch<D, 4, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-        }
-        if (nw == 8) {
-            // FA2_TUNE_DKDV_MF: MFMA shape, 16 (16x16x32, default: +5 % at C3 -- fewer
-            // joules per FLOP under the power cap) or 32 (32x32x16)
-            if (tune_knob("DKDV_MF", 16) == 16) {
-                // FA2_TUNE_DKDV_QM: query tiles per step (2: one barrier and staging round
-                // per 128 queries)
-                if (tune_knob("DKDV_QM", 1) == 2) return dkdv_launch_qm<D, 8, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-                return dkdv_launch<D, 8, 1, 0, true>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-            }
-            return dkdv_launch<D, 8>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-        }
-    }
-    if (nw == 2) return dkdv_launch<D, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
-    // FA2_TUNE_DKDV_MF4: 16x16x32 at 4 waves too (default; +4 % at D = 128, +7 % at small D = 64 grids)
-    if (tune_knob("DKDV_MF4", 16) == 16) return dkdv_launch<D, 4, 1, 0, true>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
+    if (nw == 2) return dkdv_launch<D, 2, false>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
 template <int D, int NW, int NKB = 2, bool M16 = false, int KS = 1>
@@ -1825,12 +1416,10 @@ hipError_t dq_launch(const float* q, const float* k, const float* v, const float
                      float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
     const long grid = (long)bh * ((S + 32 * (NW / KS) - 1) / (32 * (NW / KS)));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-#if FA2_BWD_COAL
     if (o)
         hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB, M16, KS>), dim3((unsigned)grid),
                            dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     else
-#endif
         hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB, M16, KS>), dim3((unsigned)grid),
                            dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     return hipGetLastError();
@@ -1838,15 +1427,15 @@ hipError_t dq_launch(const float* q, const float* k, const float* v, const float
 template <int D>
 hipError_t dq_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                        float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
-    // 8 waves (2 per SIMD) for D <= 64; at D = 128 8 waves spill (~120 VGPRs), so 4
-    // FA2_TUNE_DQ_WAVES = 0 (default): auto_waves over the grid of 32-query wave units
-    int nw = tune_knob("DQ_WAVES", 0);
+    // 8 waves (2 per SIMD) for D <= 64; at D = 128 8 waves spill (~120 VGPRs), so 4.
+    // Launch-plan overrides (fa2_tune_set, tests and tools only): DQ_WAVES, DQ_KS.
+    int nw = tune_knob("DQ_WAVES", 0);  // 0 = auto_waves over the grid of 32-query wave units
     // (D = 128 at 8 waves spills even with 32-key tiles: Q, dO fragments, the -LSE / -Δ
     // seeds and the dQ accumulators alone are 160 VGPRs -- r01)
     // (D = 128 at 8 waves on 16x16x32 with 32-key tiles still spills ~70 VGPRs inside the
     // loop: Q, dO fragments and the dQ accumulators alone take 128)
     const long units = (long)bh * ((S + 31) / 32);
-    // FA2_TUNE_DQ_KS: key groups per workgroup (0 = auto).  Auto, at 8 waves: KS = 2
+    // Key groups per workgroup (0 = auto).  Auto, at 8 waves: KS = 2
     // below 8 query blocks per CU, KS = 4 below 4 (KS = 4 runs 32-key tiles: 64-key
     // tiles with the 4-tile staging registers spill).  Measured (B2_H8_D64 dQ + Δ,
     // r01): S = 512 17.0 -> 11.4 us, 1024 29.5 -> 15.7, 2048 41.9 -> 36.7.
@@ -1863,17 +1452,12 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
         if (ksp == 2 && nw == 4) return dq_launch<D, 4, 2, true, 2>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
         if (ksp == 4 && nw == 4) return dq_launch<D, 4, 1, true, 4>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
     }
-    // FA2_TUNE_DQ_MF: MFMA shape, 16 (16x16x32, default: +2.4 % at C3) or 32 (32x32x16)
-    const bool m16 = tune_knob("DQ_MF", 16) == 16;
+    // 16x16x32 (+2.4 % at C3 over 32x32x16) but at 2 waves
     if constexpr (D <= 64) {
-        if (nw == 8) {
-            if (m16) return dq_launch<D, 8, 2, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
-            return dq_launch<D, 8>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
-        }
+        if (nw == 8) return dq_launch<D, 8, 2, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
         if (nw == 2) return dq_launch<D, 2>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
     }
-    if (m16) return dq_launch<D, 4, 2, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
-    return dq_launch<D, 4>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
+    return dq_launch<D, 4, 2, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
 }
 }  // namespace
 
@@ -1914,7 +1498,6 @@ hipError_t FA2_TILE_LAUNCH(launch_bwd_dq_delta)(int D, const float* q, const flo
 }
 
 namespace {
-#ifndef FA2_STAMPS
 template <int D, int NW, int QS, int KS, int NKB>
 hipError_t fused_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                         const float* delta, float* dq, float* dk, float* dv, int bh, int S, hipStream_t stream) {
@@ -1925,17 +1508,13 @@ hipError_t fused_launch(const float* q, const float* k, const float* v, const fl
                        dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, dk, dv, S, (int)ndk);
     return hipGetLastError();
 }
-#endif
 // The fused dK/dV + dQ launch for D <= 64, or hipErrorNotSupported (then the caller
 // runs the two kernels).  Split factors follow the separate kernels' auto rule:
 // below 4 blocks of 32 rows per CU QS = 2 / KS = 4 (32-key tiles), below 8 QS = 2 /
-// KS = 2, else unsplit.  FA2_TUNE_BWD_FQS / FA2_TUNE_BWD_FKS force them.
+// KS = 2, else unsplit.  Overrides (fa2_tune_set): BWD_FQS, BWD_FKS, BWD_FNW.
 template <int D>
 hipError_t fused_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                           const float* delta, float* dq, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-#ifdef FA2_STAMPS
-    return hipErrorNotSupported;
-#else
     if constexpr (D > 64) {
         return hipErrorNotSupported;
     } else {
@@ -1946,7 +1525,7 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
         const bool tiny = a == 2 && auto_waves(units, 2, 1) == 1;
         const int fqs = tune_knob("BWD_FQS", a == 8 ? 1 : 2);
         const int fks = tune_knob("BWD_FKS", a == 8 ? 1 : (a == 4 || tiny) ? 2 : 4);
-        // FA2_TUNE_BWD_FNW: waves per workgroup of both roles (8, or 4 for the split pairs)
+        // waves per workgroup of both roles (8, or 4 for the split pairs)
         const int fnw = tune_knob("BWD_FNW", tiny ? 4 : 8);
         if (fqs == 1 && fks == 1) return fused_launch<D, 8, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
         if (fnw == 4) {
@@ -1959,7 +1538,6 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
         if (fqs == 2 && fks == 4) return fused_launch<D, 8, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
         return hipErrorNotSupported;
     }
-#endif
 }
 }  // namespace
 
@@ -1974,7 +1552,7 @@ hipError_t FA2_TILE_LAUNCH(launch_bwd_fused)(int D, const float* q, const float*
     }
 }
 
-// FA2_TUNE_BWD_FUSED: 1 = Δ kernel, then dK/dV and dQ in one launch (D <= 64);
+// Override BWD_FUSED (fa2_tune_set): 1 = Δ kernel, then dK/dV and dQ in one launch (D <= 64);
 // 0 = Δ fused into the dQ kernel's prologue (which stages dO anyway), then dK/dV,
 // which reads it; -1 (default) = 1 on grids of fewer than 8 blocks of 32 rows per
 // CU.  Measured (fwd + bwd step, B2_H8_D64, r01): S = 512 31.1 -> 27.0 us, 1024

@@ -121,9 +121,10 @@ hipError_t launch_bwd_dq_delta_bf16(int D, const float* q, const float* k, const
 
 inline bool supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
-// Launch-geometry knob read from the environment at each launch (FA2_TUNE_<NAME>=value),
-// used to A/B kernel variants in one process (tools/kbench.py); `dflt` is the
-// measured best and what ships.
+// Launch-plan override `name` as set by fa2_tune_set (include/fa2_amd.h), else `dflt`
+// (the measured best, what ships).  Never read from the environment: with no override
+// set this is one relaxed atomic load.  Tests use it to reach every instance; tools
+// use it to A/B plans in one process (tools/kbench.py).
 int tune_knob(const char* name, int dflt);
 
 // Waves per workgroup for a grid of `blocks32` 32-row wave units: the largest of

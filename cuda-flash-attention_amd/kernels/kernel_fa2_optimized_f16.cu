@@ -25,10 +25,6 @@
 // cp.RawModule path, test_flash_attention2.py:113-126), C++14 only.
 #ifndef CUPY_INLINE_COMPILE
 #include "f-attn2.cuh"
-#ifdef FA2_STAMPS
-#include <cstdio>
-#include <vector>
-#endif
 #endif
 
 #ifdef FA2_TILE_BF16
@@ -97,7 +93,7 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 // kinds are bank-conflict-free: ds_read_b128 row fragments (lane -> row) and
 // ds_read_b64_tr_b16 transposed fragments.  The backward file's swizzle is also
 // conflict-free for the 16x16x32 maps its default kernels use; this forward's
-// default kernel is 32x32x16 (fa2_fwd16_kernel's row reads are 2-way here).  f reads
+// default kernel is 32x32x16 (a 16x16x32 forward's row reads are 2-way here).  f reads
 // row bits 0..3 only: fragment offsets are computed once per lane and shifted by
 // whole 16-row blocks (FragOffsets*::rowop / trop add r0 * D).
 template <int D> struct Swz;
@@ -288,16 +284,9 @@ __device__ __forceinline__ f32x16 splat16(float x) {
 // on the lane), relative to m.  Each K fragment read from LDS feeds MQ MFMAs.
 // SEED: the chain starts from -m (scores relative to m); otherwise from 0 and the
 // softmax subtracts m per score (32-key tiles at D = 128, 16 registers fewer).
-template <int D, int MQ, int ABL = 0, int NKB = 2, bool SEED = true>
+template <int D, int MQ, int NKB = 2, bool SEED = true>
 __device__ __forceinline__ void fwd_qk(f32x16 (&s)[MQ][NKB], const FwdState<D> (&st)[MQ], const _Float16* Ks,
                                        const FragOffsets<D>& fo) {
-    if (ABL & 16) {
-#pragma unroll
-        for (int g = 0; g < MQ; ++g)
-#pragma unroll
-            for (int kb = 0; kb < NKB; ++kb) s[g][kb] = st[g].nm + fo.rowop(Ks, 0, 0)[kb];
-        return;
-    }
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
         const f16x8 a0 = fo.rowop(Ks, kb * 32, 0);
@@ -330,26 +319,16 @@ __device__ __forceinline__ float tile_max(const f32x16 (&t)[NKB]) {
     return fmaxf(fmaxf(c[0], c[1]), fmaxf(c[2], c[3]));
 }
 
-// p = exp2(s - m - sh) of the tile, packed to fp16, with its four partial row sums.
-// FA2_FWD_PKSUM: the four partial row sums as 0 = scalar f32 adds (one issue per
-// score), 1 = two float2 chains (v_pk_add_f32; at C3 the pairing spilled 15 VGPRs),
-// 2 = v_dot2 of the packed tile values against ones (one issue per two scores).
-#ifndef FA2_FWD_PKSUM
-#define FA2_FWD_PKSUM 2
-#endif
-template <bool SHIFT, int ABL = 0, int NKB = 2>
+// p = exp2(s - m - sh) of the tile, packed to fp16, with its four partial row sums:
+// v_dot2 of the packed tile values against ones (one issue per two scores, and l
+// sums exactly the P the PV MFMAs multiply; scalar f32 adds cost one issue per score,
+// and float2 chains (v_pk_add_f32) spilled 15 VGPRs at C3 -- r01)
+template <bool SHIFT, int NKB = 2>
 __device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[NKB], float sh, f16x8 (&pf)[NKB][2], float (&ls)[4]) {
-#if FA2_FWD_PKSUM == 2
-    // the row sums from the packed fp16 probabilities (v_dot2 against ones: one issue
-    // per two scores, and l sums exactly the P the PV MFMAs multiply)
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float x = SHIFT ? sacc[kb][i] - sh : sacc[kb][i];
-            const float p = (ABL & 2) ? x : fast_exp2(x);
-            pf[kb][i >> 3][i & 7] = to_tile(p);
-        }
+        for (int i = 0; i < 16; ++i) pf[kb][i >> 3][i & 7] = to_tile(fast_exp2(SHIFT ? sacc[kb][i] - sh : sacc[kb][i]));
 #pragma unroll
     for (int c = 0; c < 4; ++c) ls[c] = 0.f;
 #pragma unroll
@@ -359,44 +338,13 @@ __device__ __forceinline__ void fwd_exp(const f32x16 (&sacc)[NKB], float sh, f16
             const int c = (kb * 8 + j) & 3;
             ls[c] = pair_sum(pf[kb][j >> 2][2 * (j & 3)], pf[kb][j >> 2][2 * (j & 3) + 1], ls[c]);
         }
-#elif FA2_FWD_PKSUM
-    f32x2 acc[2];
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-            f32x2 x = {sacc[kb][i], sacc[kb][i + 1]};
-            if (SHIFT) x -= sh;
-            const f32x2 p = (ABL & 2) ? x : f32x2{fast_exp2(x[0]), fast_exp2(x[1])};
-            if (kb == 0 && i < 4) acc[i >> 1] = p;
-            else acc[(i >> 1) & 1] += p;
-            pf[kb][i >> 3][i & 7] = to_tile(p[0]);
-            pf[kb][i >> 3][(i & 7) + 1] = to_tile(p[1]);
-        }
-    ls[0] = acc[0][0];
-    ls[1] = acc[0][1];
-    ls[2] = acc[1][0];
-    ls[3] = acc[1][1];
-#else
-#pragma unroll
-    for (int c = 0; c < 4; ++c) ls[c] = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float x = SHIFT ? sacc[kb][i] - sh : sacc[kb][i];
-            const float p = (ABL & 2) ? x : fast_exp2(x);
-            ls[i & 3] += p;
-            pf[kb][i >> 3][i & 7] = to_tile(p);
-        }
-#endif
 }
 
 // Online softmax of one tile for the wave's MQ query groups (sacc = s - m) and
 // O^T += V^T P^T with the packed scores as the B operand (each V^T fragment feeds MQ
 // MFMAs).  first: the wave's first tile (m := its row max).  One slow-path decision
 // for all groups keeps the tile a single basic block on the common path.
-template <int D, int MQ, bool MASK, int ABL = 0, int NKB = 2, bool SEED = true>
+template <int D, int MQ, bool MASK, int NKB = 2, bool SEED = true>
 __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&sacc)[MQ][NKB], const _Float16* Vs,
                                                const FragOffsets<D>& fo, int k0, int S, int h, bool first) {
     if (MASK) {  // ragged last tile only
@@ -427,10 +375,7 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
                 for (int s = 0; s < 2; ++s) {
                     const f16x8 v = fo.trop(Vs, kb * 32 + 16 * s, b);
 #pragma unroll
-                    for (int g = 0; g < MQ; ++g) {
-                        if (ABL & 8) st[g].oacc[b][s + 2 * kb] += (float)pf[g][kb][s][b] + (float)v[0];
-                        else st[g].oacc[b] = mfma(v, pf[g][kb][s], st[g].oacc[b]);
-                    }
+                    for (int g = 0; g < MQ; ++g) st[g].oacc[b] = mfma(v, pf[g][kb][s], st[g].oacc[b]);
                 }
     };
     bool slow = first;
@@ -438,11 +383,11 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
         bool bad = false;
 #pragma unroll
         for (int g = 0; g < MQ; ++g) {
-            fwd_exp<!SEED, ABL, NKB>(sacc[g], st[g].m, pf[g], ls[g]);
+            fwd_exp<!SEED, NKB>(sacc[g], st[g].m, pf[g], ls[g]);
             const float ts = (ls[g][0] + ls[g][1]) + (ls[g][2] + ls[g][3]);
             bad = bad || !(ts <= FA2_TILE_SUM_MAX);
         }
-        slow = !(ABL & 32) && __any(bad);
+        slow = __any(bad);
     }
     if (slow) {
 #pragma unroll
@@ -458,7 +403,7 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
 #pragma unroll
                 for (int i = 0; i < 16; ++i) st[g].oacc[b][i] *= alpha;
             if (SEED) st[g].nm = splat16(-st[g].m);
-            fwd_exp<true, ABL, NKB>(sacc[g], SEED ? d : st[g].m, pf[g], ls[g]);
+            fwd_exp<true, NKB>(sacc[g], SEED ? d : st[g].m, pf[g], ls[g]);
         }
         accumulate();
     } else {
@@ -514,153 +459,44 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 // the per-block fixed cost from ~20 to ~16 us at C3 but ran the tile loop ~8 %
 // slower back-to-back, a net loss on the bench step -- r01)
 //
-// ABL: timing ablations only (tools/kbench.py, -DFA2_ABLATIONS builds; results
-// are wrong when set): 1 no staging in the loop, 2 no exp, 4 no barrier, 8 no PV
-// MFMAs, 16 no QK^T MFMAs, 32 never take the slow path, 64 one KV tile only.
-// FA2_FWD_LP: 0 = the next tile's global loads at the tile start, 1 = after QK^T
-// (guide T14: the eight waves' loads then queue on the texture unit under the
-// softmax instead of stalling every wave at the tile start)
-#ifndef FA2_FWD_LP
-#define FA2_FWD_LP 1
-#endif
-#ifndef FA2_FWD_SW
-#define FA2_FWD_SW 0
-#endif
-// FA2_FWD_COAL: Q loaded and O stored as whole rows through LDS (prologue/epilogue)
-#ifndef FA2_FWD_COAL
-#define FA2_FWD_COAL 1
-#endif
-
-// FA2_STAMPS (diagnostic builds only): s_memtime at the loop's segment boundaries,
-// per-wave sums written to `stamps` (read the shares, never the build's run time:
-// the stamps' fences forbid overlaps the real kernel has; guide §7 'In-kernel stamps').
-#ifdef FA2_STAMPS
-#define FA2_NSTAMP 5
-#define FA2_STAMP(k)                                                                              \
-    do {                                                                                          \
-        __builtin_amdgcn_sched_barrier(0);                                                        \
-        unsigned long long t_;                                                                    \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
-        __builtin_amdgcn_sched_barrier(0);                                                        \
-        stv[k] += t_ - tprev;                                                                     \
-        tprev = t_;                                                                               \
-    } while (0)
-#define FA2_STAMP_ARG , unsigned long long* __restrict__ stamps
-#define FA2_STAMPS_ON 1
-#else
-#define FA2_STAMPS_ON 0
-#define FA2_STAMP(k)
-#define FA2_STAMP_ARG
-#endif
-
-// FA2_FWD_STAG (8-wave workgroups): waves 4-7 run half a tile behind waves 0-3.
-// The two waves of a SIMD (w, w + 4) run the same program, and the per-tile barrier
-// kept them in lockstep: both in QK^T (MFMA) together, then both in the softmax
-// (VALU) together.  Staggered, the lagging wave finishes tile j-1 (softmax + PV)
-// while its partner computes QK^T of tile j, and runs its own QK^T of tile j while
-// the partner is in the softmax (guide MI355X_MICROARCH §Two waves per SIMD, item 9).
-// V of tile j-1 is read one interval later, so the K/V ring has three slots.
-#ifndef FA2_FWD_STAG
-#define FA2_FWD_STAG 0
-#endif
-// FA2_FWD_PRIO: s_setprio 1 for waves 4-7 of an 8-wave workgroup for the whole loop
-// (the second-dispatched half loses VALU arbitration by age; guide item 4)
-#ifndef FA2_FWD_PRIO
-#define FA2_FWD_PRIO 1
-#endif
-// FA2_FWD_W4_OCC: waves per SIMD the 4-wave kernel is register-budgeted for (2: two
-// independent 4-wave workgroups per CU, whose SIMD partners share no barrier)
-#ifndef FA2_FWD_W4_OCC
-#define FA2_FWD_W4_OCC 1
-#endif
-
-template <int N>
-struct Slot {
-    static constexpr int value = N;
-};
-
-// The tile loop of a staggered workgroup: ONE body for both halves (one register
-// allocation), iteration i = { load tile i+1; softmax + PV of tile i-1; QK^T of
-// tile i; store tile i+1 }, with the barrier placed per half:
-//   leading half (waves 0..NW/2-1): before QK^T (from i = 1), and once after the
-//     final softmax -> interval k holds its QK^T(k-1), softmax(k-1);
-//   lagging half: after the store -> interval k holds its softmax(k-2), QK^T(k-1).
-// Both halves store tile k in interval k into slot k % 3 while the workgroup reads
-// slots (k-1) % 3 and (k-2) % 3 only.  S^T of tile i is carried into iteration
-// i+1; QK^T of tile i always follows the softmax of tile i-1 (it reads -m), so the
-// arithmetic, and the outputs, are those of the unstaggered loop.
-template <int D, int MQ, int ABL, int NKB, bool SEED, class Stager>
-__device__ __forceinline__ void fwd_loop_stag(FwdState<D> (&st)[MQ], _Float16* smem, const FragOffsets<D>& fo,
-                                              Stager& ks, Stager& vs, int ntiles, int last_ragged, int S, int h,
-                                              int tid, bool lead) {
-    constexpr int KT = 32 * NKB;
-    constexpr int TILE = KT * D;
-    f32x16 sprev[MQ][NKB];
-    auto softmax = [&](const _Float16* Vs, int j) {
-        if (j == last_ragged) fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sprev, Vs, fo, j * KT, S, h, j == 0);
-        else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sprev, Vs, fo, j * KT, S, h, j == 0);
-    };
-    auto step = [&](auto slot, int i) {
-        constexpr int sc = decltype(slot)::value, sp = (sc + 2) % 3, sn = (sc + 1) % 3;
-        const bool more = !(ABL & 1) && i + 1 < ntiles;
-        if (more) {
-            ks.load((i + 1) * KT);
-            vs.load((i + 1) * KT);
-        }
-        if (i > 0) softmax(smem + (2 * sp + 1) * TILE, i - 1);
-        if (lead && i > 0 && !(ABL & 4)) __syncthreads();
-        fwd_qk<D, MQ, ABL, NKB, SEED>(sprev, st, smem + 2 * sc * TILE, fo);
-        if (more) {
-            ks.store(smem + 2 * sn * TILE, 1.f, tid);
-            vs.store(smem + (2 * sn + 1) * TILE, 1.f, tid);
-        }
-        if (!lead && !(ABL & 4)) __syncthreads();
-    };
-    for (int i = 0; i < ntiles; i += 3) {
-        step(Slot<0>{}, i);
-        if (i + 1 < ntiles) step(Slot<1>{}, i + 1);
-        if (i + 2 < ntiles) step(Slot<2>{}, i + 2);
-    }
-    softmax(smem + (2 * ((ntiles - 1) % 3) + 1) * TILE, ntiles - 1);
-    if (lead && !(ABL & 4)) __syncthreads();
-}
-
-// MQ 32-row query groups per wave (MQ = 2: two independent MFMA / softmax chains
-// per wave for the scheduler to interleave, each K / V^T fragment feeding two MFMAs).
+// The next tile's global loads are issued after the tile's QK^T MFMAs (guide T14:
+// issued at the tile start, the eight waves' loads queue on the texture unit and
+// stall every wave), its LDS stores after the softmax; Q is loaded and O stored as
+// whole rows through LDS (prologue / epilogue).  Waves 4-7 of an 8-wave workgroup
+// run at s_setprio 1 for the whole loop (the second-dispatched half loses VALU
+// arbitration by age; MI355X_MICROARCH §Two waves per SIMD, item 4: +0.9 %).
+//
 // NKB 32-key blocks per KV tile (2: 64-key tiles; 1: 32-key tiles, fewer registers
 // for D = 128 at 8 waves).
 //
-// KS > 1 (small grids, MQ = 1): the key range is split over KS wave groups of NQ =
-// NW / KS waves.  Wave w handles query rows of slot w % NQ against tiles j·KS + w / NQ;
+// KS > 1 (small grids): the key range is split over KS wave groups of NQ = NW / KS
+// waves.  Wave w handles query rows of slot w % NQ against tiles j·KS + w / NQ;
 // each step stages KS tiles.  The groups' (m, l, O) meet in LDS after the loop
 // (O = Σ_g 2^(m_g - m) O_g, l likewise) and group 0 stores.  That puts NW waves on
 // NQ · 32 query rows, so a grid of few query blocks still covers every SIMD twice.
-template <int D, int NW, int MQ, int ABL = 0, int NKB = 2, int KS = 1>
-__global__ void __launch_bounds__(64 * NW, (NW == 4 && D <= 64) ? FA2_FWD_W4_OCC : 1)
+template <int D, int NW, int NKB = 2, int KS = 1>
+__global__ void __launch_bounds__(64 * NW)
 fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                   float* __restrict__ O, float* __restrict__ LSE, int S FA2_STAMP_ARG) {
+                   float* __restrict__ O, float* __restrict__ LSE, int S) {
+    constexpr int MQ = 1;            // query groups per wave (2 measured -30 % at D = 32/64: r01)
     constexpr bool SEED = NKB == 2;  // -m seed for 64-key tiles; 32-key tiles subtract m
     constexpr int KT = 32 * NKB;  // keys per tile
     constexpr int NT = 64 * NW;
     constexpr int TILE = KT * D;
     constexpr int QW = 32 * MQ;  // query rows per wave
-    static_assert(KS == 1 || (MQ == 1 && !FA2_STAMPS_ON && NW % KS == 0), "key split: MQ = 1");
+    static_assert(NW % KS == 0, "key split");
     constexpr int NQ = NW / KS;  // query waves (KS > 1: waves w, w + NQ, ... share rows)
-    constexpr bool STAG = FA2_FWD_STAG && NW == 8 && NKB == 2 && KS == 1;
-    constexpr int NSLOT = STAG ? 3 : 2;
     // key-split merge records: per wave of groups 1..KS-1, O (D/2 floats per lane), m, l
     constexpr int MREC = (D / 2 + 2) * 64;
     constexpr int MERGE = KS > 1 ? 2 * (KS - 1) * NQ * MREC : 0;  // in halves
-    // [slot][K | V][KS] tiles; at least one Q block (coalesced prologue) and the merge
+    // [buf][K | V][KS] tiles; at least one Q block (coalesced prologue) and the merge
     // OVL: the prologue's Q block behind the first K/V buffer, loaded with the first step
     constexpr bool OVL = KS > 1;
     constexpr int QB = (OVL ? 2 * KS * TILE : 0) + 32 * MQ * NQ * D;
-    constexpr int SMEM0 = 2 * NSLOT * KS * TILE > QB ? 2 * NSLOT * KS * TILE : QB;
+    constexpr int SMEM0 = 4 * KS * TILE > QB ? 4 * KS * TILE : QB;
     constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;
     __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
-#if FA2_FWD_COAL
     __shared__ __attribute__((aligned(16))) float ostage[NQ][32][36];  // per-wave O block stage
-#endif
 
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = KS > 1 ? (tid >> 6) % NQ : tid >> 6;  // query slot of the wave
@@ -669,26 +505,19 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = bid / nqb, qb = bid - bh * nqb;
     const long base = (long)bh * S * D;
-    const int q0 = qb * QW * NQ + wave * QW + r;  // group g: query q0 + 32 g
+    const int q0 = qb * QW * NQ + wave * QW + r;
 
     FwdState<D> st[MQ];
     FragOffsets<D> fo;
     fo.init(lane);
-    // K/V staging by the first FA2_FWD_SW waves (all when 0): the second half loses
-    // VALU arbitration to its SIMD partners, so the first half takes the staging
-    constexpr int SW = (FA2_FWD_SW > 0 && FA2_FWD_SW < NW) ? FA2_FWD_SW : NW;
     // (KS > 1: a step stages KS consecutive tiles as one [KS * KT][D] image per tensor)
-    TileStager<D, KT * KS, 64 * SW> ks, vs;
+    TileStager<D, KT * KS, NT> ks, vs;
     ks.init(K + base, S, tid);
     vs.init(V + base, S, tid);
-    // (compile-time true when all waves stage: fewer branches around the loads, +0.7 %
-    // at C3, +1.9 % at C4)
-    ks.on = vs.on = SW == NW || __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
-    const int ntiles = (ABL & 64) ? 1 : (S + KT - 1) / KT;
+    const int ntiles = (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     const int nsteps = (ntiles + KS - 1) / KS;
-#if FA2_FWD_COAL
-    // Q block (32*MQ*NW rows, one contiguous HBM range) loaded row-coalesced, converted
+    // Q block (32*NQ rows, one contiguous HBM range) loaded row-coalesced, converted
     // and scaled into LDS, then read back as this wave's B fragments: 1 KB per load
     // instruction instead of 32 rows x 32 B per-lane pieces.  OVL (key split: small
     // grids, where the prologue's round trips are exposed): its loads and the first K/V
@@ -709,12 +538,9 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             vs.store(smem + KS * TILE, 1.f, tid);
         }
         __syncthreads();
+        fwd_init<D, SEED>(st[0], nullptr, 0, S, S, h);  // state only (q >= S: no Q read)
 #pragma unroll
-        for (int g = 0; g < MQ; ++g) {
-            fwd_init<D, SEED>(st[g], nullptr, 0, S, S, h);  // state only (q >= S: no Q read)
-#pragma unroll
-            for (int t = 0; t < D / 16; ++t) st[g].qf[t] = fo.rowop(qblk, wave * QW + 32 * g, t);
-        }
+        for (int t = 0; t < D / 16; ++t) st[0].qf[t] = fo.rowop(qblk, wave * QW, t);
         __syncthreads();  // every wave has its Q fragments before their buffer is restaged
     }
     // the group's tile within each staged image: folded into the per-lane offsets, so
@@ -727,93 +553,33 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         vs.store(smem + KS * TILE, 1.f, tid);
         __syncthreads();
     }
-#else
-#pragma unroll
-    for (int g = 0; g < MQ; ++g) fwd_init<D, SEED>(st[g], Q, base, q0 + 32 * g, S, h);
-    if (KS > 1) fo.shift(kg * TILE);
-    ks.load(0);
-    vs.load(0);
-    ks.store(smem, 1.f, tid);
-    vs.store(smem + KS * TILE, 1.f, tid);
-    __syncthreads();
-#endif
 
-    if (FA2_FWD_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    if constexpr (STAG) {
-        fwd_loop_stag<D, MQ, ABL, NKB, SEED>(st, smem, fo, ks, vs, ntiles, last_ragged, S, h, tid,
-                                             __builtin_amdgcn_readfirstlane(wave) < NW / 2);
-    } else {
-#ifdef FA2_STAMPS
-    unsigned long long stv[FA2_NSTAMP] = {0, 0, 0, 0, 0}, tprev;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tprev)::"memory");
-#endif
+    if (NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    // one staged step out of the current buffers; the next step's loads after QK^T
+    auto step = [&](const _Float16* Kc, const _Float16* Vc, _Float16* Kn, _Float16* Vn, int j, bool more) {
+        const int jj = j * KS + kg;                // this wave's tile
+        const bool live = KS == 1 || jj < ntiles;  // wave-uniform (KS > 1: ragged tail)
+        f32x16 sacc[MQ][NKB];
+        if (live) fwd_qk<D, MQ, NKB, SEED>(sacc, st, Kc, fo);
+        if (more) {
+            ks.load((j + 1) * KS * KT);
+            vs.load((j + 1) * KS * KT);
+        }
+        if (live) {
+            if (jj == last_ragged) fwd_softmax_pv<D, MQ, true, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h, j == 0);
+            else fwd_softmax_pv<D, MQ, false, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h, j == 0);
+        }
+        if (more) {
+            ks.store(Kn, 1.f, tid);
+            vs.store(Vn, 1.f, tid);
+        }
+        __syncthreads();
+    };
     // two steps per trip so every LDS buffer offset is a compile-time immediate
     for (int j = 0; j < nsteps; j += 2) {
-        {
-            const bool more = !(ABL & 1) && j + 1 < nsteps;
-            const int jj = j * KS + kg;             // this wave's tile
-            const bool live = KS == 1 || jj < ntiles;  // wave-uniform (KS > 1: ragged tail)
-            if (more && !FA2_FWD_LP) {
-                ks.load((j + 1) * KS * KT);
-                vs.load((j + 1) * KS * KT);
-            }
-            FA2_STAMP(0);
-            f32x16 sacc[MQ][NKB];
-            if (live) fwd_qk<D, MQ, ABL, NKB, SEED>(sacc, st, smem, fo);
-            if (more && FA2_FWD_LP) {
-                ks.load((j + 1) * KS * KT);
-                vs.load((j + 1) * KS * KT);
-            }
-            FA2_STAMP(1);
-            if (live) {
-                if (jj == last_ragged)
-                    fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sacc, smem + KS * TILE, fo, jj * KT, S, h, j == 0);
-                else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sacc, smem + KS * TILE, fo, jj * KT, S, h, j == 0);
-            }
-            FA2_STAMP(2);
-            if (more) {
-                ks.store(smem + 2 * KS * TILE, 1.f, tid);
-                vs.store(smem + 3 * KS * TILE, 1.f, tid);
-            }
-            FA2_STAMP(3);
-            if (!(ABL & 4)) __syncthreads();
-            FA2_STAMP(4);
-        }
-        if (j + 1 < nsteps) {
-            const bool more = !(ABL & 1) && j + 2 < nsteps;
-            const int jj = (j + 1) * KS + kg;
-            const bool live = KS == 1 || jj < ntiles;
-            if (more && !FA2_FWD_LP) {
-                ks.load((j + 2) * KS * KT);
-                vs.load((j + 2) * KS * KT);
-            }
-            FA2_STAMP(0);
-            f32x16 sacc[MQ][NKB];
-            if (live) fwd_qk<D, MQ, ABL, NKB, SEED>(sacc, st, smem + 2 * KS * TILE, fo);
-            if (more && FA2_FWD_LP) {
-                ks.load((j + 2) * KS * KT);
-                vs.load((j + 2) * KS * KT);
-            }
-            FA2_STAMP(1);
-            if (live) {
-                if (jj == last_ragged)
-                    fwd_softmax_pv<D, MQ, true, ABL, NKB, SEED>(st, sacc, smem + 3 * KS * TILE, fo, jj * KT, S, h, false);
-                else fwd_softmax_pv<D, MQ, false, ABL, NKB, SEED>(st, sacc, smem + 3 * KS * TILE, fo, jj * KT, S, h, false);
-            }
-            FA2_STAMP(2);
-            if (more) {
-                ks.store(smem, 1.f, tid);
-                vs.store(smem + KS * TILE, 1.f, tid);
-            }
-            FA2_STAMP(3);
-            if (!(ABL & 4)) __syncthreads();
-            FA2_STAMP(4);
-        }
-    }
-#ifdef FA2_STAMPS
-    if (lane == 0)
-        for (int k = 0; k < FA2_NSTAMP; ++k) stamps[((long)blockIdx.x * NW + wave) * FA2_NSTAMP + k] = stv[k];
-#endif
+        step(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, j, j + 1 < nsteps);
+        if (j + 1 < nsteps)
+            step(smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j + 1, j + 2 < nsteps);
     }
     if constexpr (KS > 1) {
         // Key-split merge (the loop ended on a barrier: the tile buffers are free).
@@ -848,19 +614,17 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         st[0].l[0] = l;
         st[0].l[1] = st[0].l[2] = st[0].l[3] = 0.f;
     }
-#if FA2_FWD_COAL
     // O through a wave-private LDS stage, one 32x32 block at a time, stored as whole
     // 128-B row segments (8 rows per instruction) instead of 16-B pieces of 32 rows
-#pragma unroll
-    for (int g = 0; g < MQ; ++g) {
-        const float lt = xor32_sum((st[g].l[0] + st[g].l[1]) + (st[g].l[2] + st[g].l[3]));
+    {
+        const float lt = xor32_sum((st[0].l[0] + st[0].l[1]) + (st[0].l[2] + st[0].l[3]));
         const float inv = 1.f / lt;
-        const int qrow0 = qb * QW * NQ + wave * QW + 32 * g;  // first row of this group
+        const int qrow0 = qb * QW * NQ + wave * QW;  // first row of this wave
         float(*os)[36] = ostage[wave];
 #pragma unroll
         for (int b = 0; b < D / 32; ++b) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) os[r][(i & 3) + 8 * (i >> 2) + 4 * h] = st[g].oacc[b][i] * inv;
+            for (int i = 0; i < 16; ++i) os[r][(i & 3) + 8 * (i >> 2) + 4 * h] = st[0].oacc[b][i] * inv;
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
@@ -870,272 +634,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             }
             __builtin_amdgcn_wave_barrier();
         }
-        if (h == 0 && q0 + 32 * g < S) LSE[(long)bh * S + q0 + 32 * g] = st[g].m * FA2_LN2 + __logf(lt);
-    }
-#else
-#pragma unroll
-    for (int g = 0; g < MQ; ++g) fwd_store<D>(st[g], O, LSE, base, (long)bh * S, q0 + 32 * g, S, h);
-#endif
-}
-
-// ---------------------------------------------------------------------------
-// forward on v_mfma_f32_16x16x32 (FA2_TUNE_FWD_MF=16).  Same algorithm as
-// fa2_fwd_f16_kernel (transposed S, -m seed, tile-sum overflow check); the wave's
-// 32 queries are two 16-query blocks nb, a KT-key tile is 2 NKB 16-key blocks mb.
-// Operand maps (lane l, g = l >> 4): A[m = l & 15][k = 8g + j], B[k = 8g + j][n = l & 15],
-// C[m = 4g + i][n = l & 15].
-//   S^T (m = key, n = query, k = d): A = K rows, B = Q fragments in VGPRs, seed -m.
-//   O^T (m = d, n = query, k = key): B = P^T packed k-slot j <-> key 16 (j >> 2) +
-//     4g + (j & 3) of each 32-key step; A = V^T by two 4-row transposed reads.
-// A query row is spread over lanes l, l ^ 16, l ^ 32, l ^ 48 (4 keys each per block):
-// the row max (slow path only) and the final row sum reduce over xor 16 and xor 32.
-// ---------------------------------------------------------------------------
-template <int D>
-struct FragOffsets16 {
-    int row[D / 32];
-    int tr[D / 16][2];
-    __device__ __forceinline__ void init(int lane) {
-        const int i = lane & 15, g = lane >> 4, q = i >> 2, p4 = i & 3;
-#pragma unroll
-        for (int ks = 0; ks < D / 32; ++ks) row[ks] = tile_off<D>(i, 32 * ks + 8 * g);
-#pragma unroll
-        for (int md = 0; md < D / 16; ++md) {
-            tr[md][0] = tile_off<D>(4 * g + q, 16 * md + 4 * p4);
-            tr[md][1] = tile_off<D>(16 + 4 * g + q, 16 * md + 4 * p4);
-        }
-    }
-    __device__ __forceinline__ f16x8 rowop(const _Float16* tile, int r0, int ks) const {
-        return lds_row8(tile + row[ks] + r0 * D);
-    }
-    __device__ __forceinline__ f16x8 trop(const _Float16* tile, int r0, int md) const {
-        return cat4(lds_tr4(tile + tr[md][0] + r0 * D), lds_tr4(tile + tr[md][1] + r0 * D));
-    }
-};
-
-__device__ __forceinline__ float xor16_max(float x) { return fmaxf(x, __shfl_xor(x, 16)); }
-__device__ __forceinline__ float xor16_sum(float x) { return x + __shfl_xor(x, 16); }
-
-template <int D>
-struct Fwd16State {
-    f16x8 qf[2][D / 32];    // [nb][ks]: Q (scaled) [query 16 nb + (l&15)][d 32 ks + 8g ..]
-    f32x4 oacc[D / 16][2];  // [md][nb]: O^T [d 16 md + 4g + i][query]
-    f32x4 nm[2];            // [nb]: splat of -m
-    float m[2], l[2];       // [nb]: running max (log2 domain), this lane's partial row sum
-};
-
-template <int D, int NKB, bool MASK>
-__device__ __forceinline__ void fwd16_tile(Fwd16State<D>& st, const _Float16* Ks, const _Float16* Vs,
-                                           const FragOffsets16<D>& fo, int k0, int S, int g, bool first) {
-    constexpr int MB = 2 * NKB;  // 16-key blocks per tile
-    f32x4 sa[MB][2];
-#pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks)
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb) {
-            const f16x8 ka = fo.rowop(Ks, 16 * mb, ks);
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) sa[mb][nb] = mfma16(ka, st.qf[nb][ks], ks == 0 ? st.nm[nb] : sa[mb][nb]);
-        }
-    if (MASK) {
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (k0 + 16 * mb + 4 * g + i >= S) sa[mb][nb][i] = -__builtin_inff();
-    }
-    f16x8 pf[NKB][2];  // [32-key step][nb]
-    float ls[2];
-    // p = exp2(s - sh) packed to fp16; the row sums by v_dot2 of the packed pairs (as in
-    // fwd_exp, FA2_FWD_PKSUM = 2), two chains per 16-query block
-    auto expo = [&](float sh) {
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-#pragma unroll
-            for (int kq = 0; kq < NKB; ++kq)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) pf[kq][nb][j] = to_tile(fast_exp2(sa[2 * kq + (j >> 2)][nb][j & 3] - sh));
-            float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-            for (int kq = 0; kq < NKB; ++kq)
-#pragma unroll
-                for (int j = 0; j < 8; j += 2) {
-                    if ((j >> 1) & 1) a1 = pair_sum(pf[kq][nb][j], pf[kq][nb][j + 1], a1);
-                    else a0 = pair_sum(pf[kq][nb][j], pf[kq][nb][j + 1], a0);
-                }
-            ls[nb] = a0 + a1;
-        }
-    };
-    bool slow = first;
-    if (!first) {
-        expo(0.f);
-        const bool bad = !(ls[0] <= FA2_TILE_SUM_MAX) || !(ls[1] <= FA2_TILE_SUM_MAX);
-        slow = __any(bad);
-    }
-    auto pv_acc = [&]() {
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) st.l[nb] += ls[nb];
-#pragma unroll
-        for (int md = 0; md < D / 16; ++md)
-#pragma unroll
-            for (int kq = 0; kq < NKB; ++kq) {
-                const f16x8 va = fo.trop(Vs, 32 * kq, md);
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb) st.oacc[md][nb] = mfma16(va, pf[kq][nb], st.oacc[md][nb]);
-            }
-    };
-    if (slow) {
-        float dd[2];
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            float mx = -__builtin_inff();
-#pragma unroll
-            for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sa[mb][nb][i]);
-            mx = xor32_max(xor16_max(mx));
-            const float d = first ? mx : fmaxf(mx, 0.f);
-            const float alpha = first ? 0.f : fast_exp2(-d);
-            st.m[nb] += d;
-            st.l[nb] *= alpha;
-#pragma unroll
-            for (int md = 0; md < D / 16; ++md) st.oacc[md][nb] *= alpha;
-            const float nmv = -st.m[nb];
-            st.nm[nb] = f32x4{nmv, nmv, nmv, nmv};
-            dd[nb] = d;
-        }
-        // p relative to the new m (sa holds s - m_old); two shifts as one expo pass
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-#pragma unroll
-            for (int kq = 0; kq < NKB; ++kq)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) pf[kq][nb][j] = to_tile(fast_exp2(sa[2 * kq + (j >> 2)][nb][j & 3] - dd[nb]));
-            float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-            for (int kq = 0; kq < NKB; ++kq)
-#pragma unroll
-                for (int j = 0; j < 8; j += 2) {
-                    if ((j >> 1) & 1) a1 = pair_sum(pf[kq][nb][j], pf[kq][nb][j + 1], a1);
-                    else a0 = pair_sum(pf[kq][nb][j], pf[kq][nb][j + 1], a0);
-                }
-            ls[nb] = a0 + a1;
-        }
-        pv_acc();
-    } else {
-        pv_acc();  // inside both branches: a join before it copies O on the common path
-    }
-}
-
-template <int D, int NW, int NKB>
-__global__ void __launch_bounds__(64 * NW)
-fa2_fwd16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                 float* __restrict__ O, float* __restrict__ LSE, int S) {
-    constexpr int KT = 32 * NKB;
-    constexpr int NT = 64 * NW;
-    constexpr int TILE = KT * D;
-    constexpr int SMEM = (4 * TILE > 32 * NW * D) ? 4 * TILE : 32 * NW * D;
-    __shared__ __attribute__((aligned(16))) _Float16 smem[SMEM];
-    __shared__ __attribute__((aligned(16))) float ostage[NW][32][36];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
-    const int nqb = (S + 32 * NW - 1) / (32 * NW);
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = bid / nqb, qb = bid - bh * nqb;
-    const long base = (long)bh * S * D;
-
-    FragOffsets16<D> fo;
-    fo.init(lane);
-    Fwd16State<D> st;
-    {
-        TileStager<D, 32 * NW, NT> qst;
-        qst.init(Q + base, S, tid);
-        qst.load(qb * 32 * NW);
-        qst.store(smem, FA2_LOG2E / __builtin_sqrtf((float)D), tid);
-        __syncthreads();
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int ks = 0; ks < D / 32; ++ks) st.qf[nb][ks] = fo.rowop(smem, wave * 32 + 16 * nb, ks);
-        __syncthreads();
-    }
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-#pragma unroll
-        for (int md = 0; md < D / 16; ++md) st.oacc[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        st.nm[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        st.m[nb] = 0.f;
-        st.l[nb] = 0.f;
-    }
-    if (FA2_FWD_PRIO && NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    TileStager<D, KT, NT> ks, vs;
-    ks.init(K + base, S, tid);
-    vs.init(V + base, S, tid);
-    const int ntiles = (S + KT - 1) / KT;
-    const int last_ragged = (S % KT) ? ntiles - 1 : -1;
-    ks.load(0);
-    vs.load(0);
-    ks.store(smem, 1.f, tid);
-    vs.store(smem + TILE, 1.f, tid);
-    __syncthreads();
-    for (int j = 0; j < ntiles; j += 2) {
-        {
-            const bool more = j + 1 < ntiles;
-            if (more) {
-                ks.load((j + 1) * KT);
-                vs.load((j + 1) * KT);
-            }
-            if (j == last_ragged) fwd16_tile<D, NKB, true>(st, smem, smem + TILE, fo, j * KT, S, g, j == 0);
-            else fwd16_tile<D, NKB, false>(st, smem, smem + TILE, fo, j * KT, S, g, j == 0);
-            if (more) {
-                ks.store(smem + 2 * TILE, 1.f, tid);
-                vs.store(smem + 3 * TILE, 1.f, tid);
-            }
-            __syncthreads();
-        }
-        if (j + 1 < ntiles) {
-            const bool more = j + 2 < ntiles;
-            if (more) {
-                ks.load((j + 2) * KT);
-                vs.load((j + 2) * KT);
-            }
-            if (j + 1 == last_ragged)
-                fwd16_tile<D, NKB, true>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, g, false);
-            else fwd16_tile<D, NKB, false>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, g, false);
-            if (more) {
-                ks.store(smem, 1.f, tid);
-                vs.store(smem + TILE, 1.f, tid);
-            }
-            __syncthreads();
-        }
-    }
-    // O rows through the wave's LDS stage (row = query), LSE by the g == 0 lanes
-    const int q0w = qb * 32 * NW + wave * 32;
-    float inv[2];
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-        const float lt = xor32_sum(xor16_sum(st.l[nb]));
-        inv[nb] = 1.f / lt;
-        const int qn = q0w + 16 * nb + i16;
-        if (g == 0 && qn < S) LSE[(long)bh * S + qn] = st.m[nb] * FA2_LN2 + __logf(lt);
-    }
-    float(*os)[36] = ostage[wave];
-#pragma unroll
-    for (int b = 0; b < D / 32; ++b) {
-#pragma unroll
-        for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-                *reinterpret_cast<f32x4*>(&os[16 * nb + i16][16 * mh + 4 * g]) = st.oacc[2 * b + mh][nb] * inv[nb];
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            const int row = 8 * s4 + (lane >> 3), c4 = (lane & 7) * 4;
-            const f32x4 v = *reinterpret_cast<const f32x4*>(&os[row][c4]);
-            if (q0w + row < S) *reinterpret_cast<f32x4*>(O + base + (long)(q0w + row) * D + 32 * b + c4) = v;
-        }
-        __builtin_amdgcn_wave_barrier();
+        if (h == 0 && q0 < S) LSE[(long)bh * S + q0] = st[0].m * FA2_LN2 + __logf(lt);
     }
 }
 
@@ -1213,92 +712,16 @@ __device__ __forceinline__ void fwd_compat_body(const float* __restrict__ Q, con
 #ifndef CUPY_INLINE_COMPILE
 namespace fa2 {
 
-#ifdef FA2_STAMPS
-// diagnostic: accumulate the per-wave segment sums of every launch, print shares at exit
-struct StampLog {
-    double sum[FA2_NSTAMP] = {};
-    long launches = 0;
-    ~StampLog() {
-        double t = 0;
-        for (double x : sum) t += x;
-        if (!launches || t <= 0) return;
-        const char* names[FA2_NSTAMP] = {"load-issue", "qk", "softmax+pv", "lds-store", "barrier"};
-        fprintf(stderr, "[fa2 stamps] fwd launches=%ld cycles/wave/launch=%.0f\n", launches, t / launches);
-        for (int k = 0; k < FA2_NSTAMP; ++k) fprintf(stderr, "[fa2 stamps]   %-12s %5.1f %%\n", names[k], 100 * sum[k] / t);
-    }
-};
-static StampLog g_stamps;
-#endif
-
-template <int D, int NW, int MQ, int ABL, int NKB = 2>
-static void fwd_f16_go(const float* q, const float* k, const float* v, float* o, float* lse, long grid, int S,
-                       hipStream_t stream) {
-#ifdef FA2_STAMPS
-    static unsigned long long* buf = nullptr;
-    static long cap = 0;
-    const long n = grid * NW * FA2_NSTAMP;
-    if (n > cap) {
-        if (buf) (void)hipFree(buf);
-        (void)hipMalloc(&buf, n * sizeof(unsigned long long));
-        cap = n;
-    }
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, MQ, ABL, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
-                       v, o, lse, S, buf);
-    std::vector<unsigned long long> h(n);
-    (void)hipStreamSynchronize(stream);
-    (void)hipMemcpy(h.data(), buf, n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-    for (long i = 0; i < n; ++i) g_stamps.sum[i % FA2_NSTAMP] += (double)h[i] / (grid * NW);
-    ++g_stamps.launches;
-#else
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, MQ, ABL, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
-                       v, o, lse, S);
-#endif
-}
-
-// key-split instances (KS > 1: NW / KS query waves per workgroup, no stamps/ablations)
-// (D = 64: 32-key tiles -- with 64-key tiles the KS-tile staging registers spill)
-template <int D, int NW, int KS, int NKB = (D <= 32 ? 2 : 1)>
-static hipError_t fwd_f16_launch_ks(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
-                                    hipStream_t stream) {
-#ifdef FA2_STAMPS
-    return hipErrorNotSupported;
-#else
+// KS > 1: NW / KS query waves per workgroup (D = 64: 32-key tiles -- with 64-key
+// tiles the KS-tile staging registers spill)
+template <int D, int NW, int KS = 1, int NKB = (KS == 1 || D <= 32 ? 2 : 1)>
+static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
+                                 hipStream_t stream) {
     const int nqb = (S + 32 * (NW / KS) - 1) / (32 * (NW / KS));
     const long grid = (long)bh * nqb;
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, 1, 0, NKB, KS>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q,
-                       k, v, o, lse, S);
-    return hipGetLastError();
-#endif
-}
-
-template <int D, int NW, int MQ = 1, int NKB = 2>
-static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
-                                 hipStream_t stream) {
-    const int nqb = (S + 32 * MQ * NW - 1) / (32 * MQ * NW);
-    const long grid = (long)bh * nqb;
-    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-#ifdef FA2_ABLATIONS
-    switch (tune_knob("FWD_ABL", 0)) {
-#define FA2_FWD_ABL(X) \
-    case X: fwd_f16_go<D, NW, MQ, X>(q, k, v, o, lse, grid, S, stream); return hipGetLastError();
-        FA2_FWD_ABL(1) FA2_FWD_ABL(2) FA2_FWD_ABL(4) FA2_FWD_ABL(8) FA2_FWD_ABL(16) FA2_FWD_ABL(24) FA2_FWD_ABL(32)
-        FA2_FWD_ABL(63) FA2_FWD_ABL(64)
-#undef FA2_FWD_ABL
-        default: break;
-    }
-#endif
-    fwd_f16_go<D, NW, MQ, 0, NKB>(q, k, v, o, lse, grid, S, stream);
-    return hipGetLastError();
-}
-
-template <int D, int NW, int NKB>
-static hipError_t fwd16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
-                               hipStream_t stream) {
-    const long grid = (long)bh * ((S + 32 * NW - 1) / (32 * NW));
-    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16::fa2_fwd16_kernel<D, NW, NKB>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k, v,
-                       o, lse, S);
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, NKB, KS>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
+                       v, o, lse, S);
     return hipGetLastError();
 }
 
@@ -1309,10 +732,11 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     // ~400 VGPRs (8 would spill and exceed the LDS budget with the Q stages)
     // (MQ = 2, two 32-row query groups per wave at 4 waves / 1 per SIMD, measured
     // 30 % slower than 8 waves x 1 group at D = 32 and 64 -- r01)
-    // FA2_TUNE_FWD_WAVES = 0 (default): auto_waves over the grid of 32-query wave units
+    // Launch-plan overrides (fa2_tune_set, tests and tools only): FWD_WAVES (0 = auto_waves
+    // over the grid of 32-query wave units), FWD_KS.
     const long units = (long)bh * ((S + 31) / 32);
     int nw = tune_knob("FWD_WAVES", 0);
-    // FA2_TUNE_FWD_KS: key groups per workgroup (0 = auto).  Auto: where even 4-wave
+    // Key groups per workgroup (0 = auto).  Auto: where even 4-wave
     // workgroups would leave CUs idle (< 4 query blocks per CU), split the key range
     // 4 ways instead of shrinking the workgroup -- 8 waves on 64 query rows, or 4 waves
     // on 32 rows below 2 query blocks per CU.  Measured (B2_H8_D64 fwd, r01):
@@ -1325,16 +749,10 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     }
     if (nw == 0) nw = auto_waves(units, 8);
     if constexpr (D <= 64) {
-        if (ks == 2 && nw == 8) return fwd_f16_launch_ks<D, 8, 2>(q, k, v, o, lse, bh, S, stream);
-        if (ks == 4 && nw == 8) return fwd_f16_launch_ks<D, 8, 4>(q, k, v, o, lse, bh, S, stream);
-        if (ks == 4 && nw == 4) return fwd_f16_launch_ks<D, 4, 4>(q, k, v, o, lse, bh, S, stream);
-        if (ks == 2 && nw == 4) return fwd_f16_launch_ks<D, 4, 2>(q, k, v, o, lse, bh, S, stream);
-    }
-    // FA2_TUNE_FWD_MF: MFMA shape, 32 (32x32x16) or 16 (16x16x32, fa2_fwd16_kernel)
-    if (tune_knob("FWD_MF", 32) == 16) {
-        constexpr int NKB16 = D <= 64 ? 2 : 1;
-        if (nw == 8) return fwd16_launch<D, 8, NKB16>(q, k, v, o, lse, bh, S, stream);
-        if (nw == 4) return fwd16_launch<D, 4, NKB16>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 2 && nw == 8) return fwd_f16_launch<D, 8, 2>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 4 && nw == 8) return fwd_f16_launch<D, 8, 4>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 4 && nw == 4) return fwd_f16_launch<D, 4, 4>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 2 && nw == 4) return fwd_f16_launch<D, 4, 2>(q, k, v, o, lse, bh, S, stream);
     }
     if constexpr (D <= 64) {
         if (nw == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);

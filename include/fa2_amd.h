@@ -110,6 +110,13 @@ int fa2_backward_host(const float* q, const float* k, const float* v, const floa
  * of `total_heads` belong to shard `index` of `shards` (contiguous, balanced). */
 int fa2_shard_range(int total_heads, int shards, int index, int* first, int* count);
 
+/* Launch-plan override (tests and tuning tools only; nothing is read from the
+ * environment).  fa2_tune_set("DKDV_QS", 2) makes the next launches use that plan
+ * where the shape allows it; fa2_tune_set(NULL, 0) clears every override.  Knobs:
+ * FWD_WAVES, FWD_KS, DKDV_WAVES, DKDV_QS, DQ_WAVES, DQ_KS, BWD_FUSED, BWD_FQS,
+ * BWD_FKS, BWD_FNW, BWD_ONEPASS (see the launchers in kernels/).  Process-wide. */
+int fa2_tune_set(const char* knob, int value);
+
 const char* fa2_last_error(void);
 int fa2_version(void); /* MAJOR*10000 + MINOR*100 + PATCH */
 int fa2_device_count(void);

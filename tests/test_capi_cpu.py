@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version():
-    assert fa2amd.version() == 10000
+    assert fa2amd.version() == 10100
 
 
 def test_invalid_arguments_rejected_without_device():
