@@ -79,17 +79,75 @@ int tune_knob(const char* name, int dflt) {
     return dflt;
 }
 
-int auto_waves(long blocks32, int maxnw, int minnw) {
-    static int ncu_cache[64] = {};
+int cu_count() {
+    static std::atomic<int> ncu_cache[64] = {};
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-        if (!ncu_cache[dev]) {
+        if (!ncu_cache[dev].load(std::memory_order_relaxed)) {
             int n = 0;
             if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-                ncu_cache[dev] = n;
+                ncu_cache[dev].store(n, std::memory_order_relaxed);
         }
-        if (ncu_cache[dev]) ncu = ncu_cache[dev];
+        if (const int c = ncu_cache[dev].load(std::memory_order_relaxed)) ncu = c;
     }
+    return ncu;
+}
+
+namespace {
+struct Workspace {
+    int device;
+    hipStream_t stream;
+    void* ptr;
+    size_t bytes;
+};
+std::mutex g_ws_mu;
+std::vector<Workspace> g_ws;
+}  // namespace
+
+void* bwd_workspace(hipStream_t stream, size_t bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    Workspace* w = nullptr;
+    for (auto& e : g_ws)
+        if (e.device == dev && e.stream == stream) w = &e;
+    if (w && w->bytes >= bytes) return w->ptr;
+    // (re)allocation: never inside a graph capture (the caller then takes another plan)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    const size_t want = std::max(bytes, w ? 2 * w->bytes : (size_t)1 << 16);
+    void* p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, want) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+    }
+    if (w) {
+        (void)hipStreamSynchronize(stream);  // the old block may still be in use there
+        (void)hipFree(w->ptr);
+        w->ptr = p;
+        w->bytes = want;
+    } else {
+        g_ws.push_back({dev, stream, p, want});
+    }
+    return p;
+}
+
+void release_workspace(hipStream_t stream) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    for (size_t i = 0; i < g_ws.size(); ++i)
+        if (g_ws[i].device == dev && g_ws[i].stream == stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipFree(g_ws[i].ptr);
+            g_ws.erase(g_ws.begin() + i);
+            return;
+        }
+}
+
+int auto_waves(long blocks32, int maxnw, int minnw) {
+    const int ncu = cu_count();
     for (int nw = maxnw; nw > minnw; nw /= 2)
         if ((blocks32 + nw - 1) / nw >= ncu) return nw;
     return minnw;
@@ -238,7 +296,10 @@ int run_shard(HostJob& j) {
     if ((rc = hip_status(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
     struct StreamGuard {
         hipStream_t s;
-        ~StreamGuard() { (void)hipStreamDestroy(s); }
+        ~StreamGuard() {
+            fa2::release_workspace(s);
+            (void)hipStreamDestroy(s);
+        }
     } sg{st};
     hipEvent_t e0, e1;
     if ((rc = hip_status(hipEventCreate(&e0), "hipEventCreate"))) return rc;

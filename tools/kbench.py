@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B kernel variants in ONE process (guide §5.4 rule 24): interleaved rounds,
-median and min per variant.  Variants are FA2_TUNE_* environment settings read
-by the launchers at every launch.
+median and min per variant.  Variants are launch-plan overrides (fa2_tune_set,
+include/fa2_amd.h) or alternate library builds.
 
   python tools/kbench.py --shape 4,16,2048,64 --kernel fwd --variant FWD_WAVES=4 --variant FWD_WAVES=8
 """
@@ -68,7 +68,7 @@ def main():
                          fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
                          fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv)),
         "dqd": lambda: fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
-        # fwd + fa2_backward (whatever launch plan launch_backward picks, e.g. FA2_TUNE_BWD_FUSED)
+        # fwd + fa2_backward (whatever launch plan launch_backward picks, e.g. BWD_ONEPASS)
         "stepb": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
                           fa2amd.backward(q, k, v, o, do, lse, "fp16", dq=dq, dk=dk, dv=dv, delta_buf=dl)),
         # dK/dV and dQ on two streams after a separate delta kernel
@@ -103,14 +103,12 @@ def main():
         if var.startswith("lib="):
             path, _, var = var[4:].partition(",")
             fa2amd.use_library(path)
-        for key in list(os.environ):
-            if key.startswith("FA2_TUNE_"):
-                del os.environ[key]
+        fa2amd.tune_set(None)
         for kv in filter(None, var.split(",")):
             if kv.startswith("lib="):
                 continue
             kk, vv = kv.split("=")
-            os.environ["FA2_TUNE_" + kk] = vv
+            fa2amd.tune_set(kk, int(vv))
 
     res = {(kn, var): [] for kn in kernels for var in variants}
     for r in range(args.rounds):
