@@ -2,32 +2,43 @@
 """bench.py -- FA2 forward+backward on MI355X, BASELINE.json's headline metric.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c5|c1]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-One *step* = the FA2 forward (O, LSE) + backward (dQ with Δ fused, dK/dV) over one batch
-of synthetic fp32 inputs already resident in HBM (harness distribution:
-torch.manual_seed(42 + rank), torch.rand for Q, K, V; dO = ones as the reference
-harness uses, test_flash_attention2.py:220-232).  Default workload is BASELINE
-config C3, B4_H16_S2048_D64, fp16 tiles on MFMA -- the config the metric is
-quoted on ("... at S=2048 D=64"), per rank: multi-GPU runs shard batch x heads,
-each rank owning its own B*H slice with no data-path collective
-(scaling "weak"; --workload c5 instead splits B64_H16_S2048_D64 over the ranks).
+One *step* = the FA2 forward (O, LSE) + backward (dQ, dK, dV; fa2_backward's launch
+plan) over one batch of synthetic fp32 inputs already resident in HBM (harness
+distribution: torch.manual_seed(42 + rank), torch.rand for Q, K, V; dO = ones as
+the reference harness uses, test_flash_attention2.py:220-232), fp16 tiles on MFMA.
 
-value = algorithmic fwd+bwd FLOPs of all ranks (14*B*H*S^2*D each) / the max over
-ranks of the K-step wall time (barrier + synchronize on both sides), the kernels
-issued back to back as a caller issues them.
-roofline = the dominant kernel's algorithmic FLOPs / its mean duration, timed
-live with HIP events recorded on the kernel's own stream around every launch of a
-second K-step region (events serialise the stream, so these are the isolated
-durations rocprofv3 reports), against the dense fp16 MFMA peak.  cpu_baseline = the C
-restatement of the oracle (oracle/fa2_oracle.c, "port") on the host cores, on a
-bounded sample of the same workload (whole heads, rank 0, N=1 only).
+Workloads (BASELINE.json configs):
+  * N = 1 (default c3): B4_H16_S2048_D64, the config the metric is quoted on
+    ("... at S=2048 D=64", the headline roofline config);
+  * N > 1 (default c5): B64_H16_S2048_D64 strong-scaled over the ranks, the
+    north star's 1/2/4/8-GPU curve: every rank takes the contiguous B*H slice
+    fa2_shard_range gives it (one process per GPU, no data-path collective;
+    RCCL only carries the timing barrier and the max over ranks).  The N = 1 line
+    also times C5 on one GPU (extra_configs.c5_1gpu) as the curve's anchor.
+`--gpus N` without a launcher starts N ranks itself (torch.distributed.run, before
+any GPU call in this process) and exits with their status.
+
+value = algorithmic fwd+bwd FLOPs of the job (14*B*H*S^2*D) / the max over ranks of
+the K-step wall time (barrier + synchronize on both sides).
+roofline = the dominant kernel launch's algorithmic FLOPs / its mean duration, timed
+live with HIP events on the launch's own stream around every launch of a second
+K-step region, against the dense fp16 MFMA peak; traffic = its HBM bytes per launch
+from the committed rocprofv3 PMC summary (profiles/pmc_summary.json).
+cpu_baseline (rank 0, N = 1) = PyTorch-CPU SDPA fwd+bwd (north_star's baseline) on
+the host's usable cores, 2 warm-ups then the median of >= 3 runs, on whole heads of
+the workload; the harness's compute_reference and the C restatement of the oracle
+(oracle/fa2_oracle.c) are timed beside it, and C1 (config #1, the reference's
+"CPU reference path") as well.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -46,14 +57,15 @@ WORKLOADS = {
     "c5": (64, 16, 2048, 64, False),
     "c1": (2, 8, 512, 64, True),
 }
+METRIC = "FA2 fwd+bwd TFLOPS & HBM GB/s (% of gfx950 roofline) at S=2048 D=64"
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-PMC_PREFIX = {"fwd": "fa2_fwd_f16", "dkdv": "fa2_bwd_dkdv_f16", "dq": "fa2_bwd_dq_f16", "delta": "fa2_delta",
-              "bwd": "fa2_bwd_f32"}
+# kernel-name prefixes in the rocprofv3 PMC summary
+PMC_PREFIX = {"fwd": "fa2_fwd_f16", "bwd": "fa2_bwd_onepass_f16", "bwd32": "fa2_bwd_f32"}
 
 
 def traffic_from_profile(kernel: str, D: int, S: int, heads: int):
@@ -78,32 +90,114 @@ def traffic_from_profile(kernel: str, D: int, S: int, heads: int):
     return None
 
 
-def cpu_baseline(S, D, sample_heads=None):
-    """Time the C oracle (fwd + bwd) on whole heads of the workload's shape."""
-    from oracle import c_oracle, fa2_oracle as fo
+# ---------------------------------------------------------------------------
+# CPU baseline
+# ---------------------------------------------------------------------------
+def usable_cpus():
+    """(cpus this process may run on: affinity capped by the cgroup CPU quota, affinity
+    count, quota or None)"""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
 
-    cores = len(os.sched_getaffinity(0))
-    threads = max(1, min(cores, 16))
-    heads = sample_heads or threads
-    q, k, v = fo.harness_inputs(1, heads, S, D, seed=42)
-    do = np.ones_like(q)
-    c_oracle.forward(q[:, :1, :64], k[:, :1, :64], v[:, :1, :64], 1)  # load/build outside the timed region
-    t0 = time.perf_counter()
-    o, lse = c_oracle.forward(q, k, v, nthreads=threads)
-    c_oracle.backward(q, k, v, o, do, lse, nthreads=threads)
-    dt = time.perf_counter() - t0
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return "unknown"
+
+
+def _median_runs(fn, warm=2, runs=3, budget_s=8.0):
+    """2 warm-ups, then >= `runs` timed runs (more while within budget); median s"""
+    for _ in range(warm):
+        fn()
+    ts = []
+    t_all = time.perf_counter()
+    while len(ts) < runs or (time.perf_counter() - t_all < budget_s and len(ts) < 10):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts), len(ts)
+
+
+def cpu_baseline(S, D, heads):
+    """PyTorch-CPU SDPA fwd+bwd on `heads` heads of (S, D) -- the north star's
+    baseline -- with the harness's compute_reference (matmul, /sqrt(D), softmax,
+    matmul; autograd with dO = ones: test_flash_attention2.py:197-232) and the
+    oracle's C port beside it; plus the C1 (B2_H8_S512_D64) fwd+bwd entry."""
+    import torch
+
+    threads, aff, quota = usable_cpus()
+    torch.set_num_threads(threads)
     flops = 14.0 * heads * S * S * D
-    return {"value": round(flops / dt / 1e12, 5), "unit": "TFLOPS", "cores": threads, "kind": "port",
-            "sample": f"{heads} heads x (S={S}, D={D}) fp32 fwd+bwd, oracle/fa2_oracle.c, {dt:.2f} s"}
+    gen = torch.Generator().manual_seed(42)
+    q, k, v = (torch.rand(1, heads, S, D, generator=gen) for _ in range(3))
+
+    def sdpa(q=q, k=k, v=v):
+        qq, kk, vv = (x.clone().requires_grad_() for x in (q, k, v))
+        o = torch.nn.functional.scaled_dot_product_attention(qq, kk, vv)
+        o.backward(torch.ones_like(o))
+
+    def compute_reference(q=q, k=k, v=v):
+        qq, kk, vv = (x.clone().requires_grad_() for x in (q, k, v))
+        s = torch.matmul(qq, kk.transpose(-2, -1)) / (D ** 0.5)
+        o = torch.matmul(torch.softmax(s, dim=-1), vv)
+        o.backward(torch.ones_like(o))
+
+    t_sdpa, n_sdpa = _median_runs(sdpa)
+    t_ref, n_ref = _median_runs(compute_reference)
+    out = {"value": round(flops / t_sdpa / 1e12, 5), "unit": "TFLOPS", "cores": threads, "kind": "reference",
+           "sample": f"{heads} heads x (S={S}, D={D}) fp32 torch SDPA fwd+bwd (autograd, dO = ones), "
+                     f"median of {n_sdpa} after 2 warm-ups: {t_sdpa:.3f} s; {threads} threads",
+           "cpu_model": cpu_model(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+           "compute_reference": {"value": round(flops / t_ref / 1e12, 5), "unit": "TFLOPS", "median_s": round(t_ref, 4),
+                                 "runs": n_ref}}
+    try:
+        from oracle import c_oracle, fa2_oracle as fo
+
+        qn, kn, vn = fo.harness_inputs(1, heads, S, D, seed=42)
+        don = np.ones_like(qn)
+        c_oracle.forward(qn[:, :1, :64], kn[:, :1, :64], vn[:, :1, :64], 1)  # load / build outside the timing
+
+        def port():
+            o, lse = c_oracle.forward(qn, kn, vn, nthreads=threads)
+            c_oracle.backward(qn, kn, vn, o, don, lse, nthreads=threads)
+
+        t_port, n_port = _median_runs(port, warm=1, runs=3, budget_s=4.0)
+        out["oracle_port"] = {"value": round(flops / t_port / 1e12, 5), "unit": "TFLOPS", "kind": "port",
+                              "median_s": round(t_port, 4), "runs": n_port, "source": "oracle/fa2_oracle.c"}
+    except Exception as e:  # reported, never required
+        log("oracle port baseline failed:", e)
+    # C1 = B2_H8_S512_D64: the reference's CPU-runnable config (#1), fwd+bwd
+    B1, H1, S1, D1 = 2, 8, 512, 64
+    q1, k1, v1 = (torch.rand(B1, H1, S1, D1, generator=gen) for _ in range(3))
+    t1, n1 = _median_runs(lambda: sdpa(q1, k1, v1))
+    out["c1_B2_H8_S512_D64"] = {"value": round(14.0 * B1 * H1 * S1 * S1 * D1 / t1 / 1e12, 5), "unit": "TFLOPS",
+                                "median_s": round(t1, 5), "runs": n1, "what": "torch SDPA fwd+bwd"}
+    return out
 
 
+# ---------------------------------------------------------------------------
+# GPU timing helpers
+# ---------------------------------------------------------------------------
 def time_config(fa2amd, torch, dev, B, H, S, D, prec, fwd_only, iters=50, warmup=3, warmup_ms=250.0, dist=None,
                 total_heads=None):
     """Mean ms of fwd (+ bwd) on one synthetic config (harness distribution), events on
     the current stream; returns (ms, tflops, gbps) with the algorithmic counts.  With
-    `dist` (multi-GPU sweep): each rank runs its own B x H slice, the region is
-    bracketed by barriers, ms is the max over ranks and the rates count
-    `total_heads` heads."""
+    `dist` each rank runs its own B x H slice, the region is bracketed by barriers, ms
+    is the max over ranks and the rates count `total_heads` heads."""
     gen = torch.Generator().manual_seed(7)
     q, k, v = (torch.rand(B, H, S, D, generator=gen).to(dev) for _ in range(3))
     do = torch.ones_like(q)
@@ -148,9 +242,9 @@ def all_max(torch, dist, dev, x):
 
 
 def roof_entry(ms, tf, gbps, S, fwd_only):
-    """A sweep point against its binding roofline: algorithmic intensity (fwd S/4,
-    fwd+bwd 14 S / 48 FLOP/B at fp32 I/O) below the fp16 MFMA ridge (peak FLOP/s over
-    HBM B/s) means HBM-bound."""
+    """A point against its binding roofline: algorithmic intensity (fwd S/4, fwd+bwd
+    14 S / 48 FLOP/B at fp32 I/O) below the fp16 MFMA ridge (peak FLOP/s over HBM B/s)
+    means HBM-bound."""
     intensity = (S / 4.0) if fwd_only else (14.0 * S / 48.0)
     ridge = MFMA_F16_PEAK_TFLOPS * 1e3 / HBM_PEAK_GBPS
     fm, fh = tf / MFMA_F16_PEAK_TFLOPS, gbps / HBM_PEAK_GBPS
@@ -164,8 +258,7 @@ SWEEP_S = (512, 1024, 2048, 4096)
 
 def sweep_sharded(fa2amd, torch, dev, dist, world, rank):
     """north_star's sweep, B2_H8_S{512..4096}_D64 fwd+bwd, with its 16 heads sharded
-    over the ranks (contiguous B x H slices, no collective on the data path): the
-    1/2/4/8-GPU points the north star asks for."""
+    over the ranks (contiguous B x H slices, no collective on the data path)."""
     first, heads = fa2amd.shard_range(16, world, rank)
     out = {}
     for S in SWEEP_S:
@@ -174,40 +267,40 @@ def sweep_sharded(fa2amd, torch, dev, dist, world, rank):
     return out
 
 
-def torch_sdpa_cpu(S, D, heads):
-    """PyTorch-CPU SDPA fwd+bwd (autograd) on the host cores: the reference harness's
-    CPU baseline (test_flash_attention2.py), timed beside the oracle port."""
-    import torch
-
-    threads = max(1, min(len(os.sched_getaffinity(0)), 16))
-    torch.set_num_threads(threads)
-    gen = torch.Generator().manual_seed(42)
-    q, k, v = (torch.rand(1, heads, S, D, generator=gen).requires_grad_() for _ in range(3))
-    t0 = time.perf_counter()
-    o = torch.nn.functional.scaled_dot_product_attention(q, k, v)
-    o.backward(torch.ones_like(o))
-    dt = time.perf_counter() - t0
-    return {"value": round(14.0 * heads * S * S * D / dt / 1e12, 5), "unit": "TFLOPS", "cores": threads,
-            "sample": f"{heads} heads x (S={S}, D={D}) fp32 torch SDPA fwd+bwd (autograd), {dt:.2f} s"}
-
-
 def extras(fa2amd, torch, dev):
-    """north_star's sweep and BASELINE.json's other GPU configs, each against its roofline."""
+    """north_star's sweep, BASELINE.json's other GPU configs (C2, C4, bf16 C3) and the
+    one-GPU anchor of the C5 scaling curve, each against its roofline."""
     out = {"sweep_B2_H8_D64_fp16_fwdbwd": {}}
     for S in SWEEP_S:
         ms, tf, gbps = time_config(fa2amd, torch, dev, 2, 8, S, 64, "fp16", False)
         out["sweep_B2_H8_D64_fp16_fwdbwd"][str(S)] = roof_entry(ms, tf, gbps, S, False)
     ms, tf, gbps = time_config(fa2amd, torch, dev, 8, 16, 4096, 128, "fp16", True, iters=20)
-    out["c4_B8_H16_S4096_D128_fp16_fwd"] = {"ms": round(ms, 4), "tflops": round(tf, 2), "hbm_gbps": round(gbps, 1),
-                                            "frac_mfma": round(tf / MFMA_F16_PEAK_TFLOPS, 4),
-                                            "frac_hbm": round(gbps / HBM_PEAK_GBPS, 4)}
+    out["c4_B8_H16_S4096_D128_fp16_fwd"] = roof_entry(ms, tf, gbps, 4096, True)
     ms, tf, gbps = time_config(fa2amd, torch, dev, 4, 16, 2048, 64, "bf16", False)
-    out["c3_B4_H16_S2048_D64_bf16_fwdbwd"] = {"ms": round(ms, 4), "tflops": round(tf, 2),
-                                              "frac_mfma": round(tf / MFMA_F16_PEAK_TFLOPS, 4)}
+    out["c3_B4_H16_S2048_D64_bf16_fwdbwd"] = roof_entry(ms, tf, gbps, 2048, False)
     ms, tf, gbps = time_config(fa2amd, torch, dev, 2, 8, 512, 64, "fp32", False)
     out["c2_B2_H8_S512_D64_fp32_fwdbwd"] = {"ms": round(ms, 4), "tflops": round(tf, 2),
                                             "frac_mfma_f32": round(tf / MFMA_F32_PEAK_TFLOPS, 4)}
+    ms, tf, gbps = time_config(fa2amd, torch, dev, 64, 16, 2048, 64, "fp16", False, iters=10)
+    out["c5_1gpu_B64_H16_S2048_D64_fp16_fwdbwd"] = roof_entry(ms, tf, gbps, 2048, False)
     return out
+
+
+# ---------------------------------------------------------------------------
+# launcher
+# ---------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`--gpus N` with no launcher: start N ranks under torch.distributed.run (as the
+    driver does) from this process, which touches no GPU, and return their status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def main():
@@ -218,42 +311,68 @@ def main():
     ap.add_argument("--warmup-ms", type=float, default=400.0,
                     help="keep warming (untimed) until at least this much wall time has passed: the "
                          "power-capped MI355X needs ~0.2 s of load to reach its steady clock")
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None,
+                    help="default: c3 on one GPU, c5 (strong-scaled) on more")
     ap.add_argument("--precision", choices=["fp16", "fp32", "bf16"], default="fp16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the S sweep / C2 / C4 extra configs")
+    ap.add_argument("--no-extras", action="store_true", help="skip the S sweep / C2 / C4 / C5 extra configs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher and rank plumbing only (gloo, no GPU work): the JSON line without numbers")
     args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0:
+        if args.gpus > 1:
+            return spawn_ranks(args.gpus)
+        world = 1
+    elif args.gpus != world:
+        log(f"--gpus {args.gpus} but WORLD_SIZE {world}: measuring the {world} launched ranks")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    workload = args.workload or ("c3" if world == 1 else "c5")
+    B, H, S, D, per_rank = WORKLOADS[workload]
 
     import torch
     import torch.distributed as dist
 
-    import fa2amd
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # FA2_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- rehearses the N > 1 path
     # (barriers, max over ranks, sharded sweep) on a one-GPU box; never used for numbers
-    rehearse = os.environ.get("FA2_BENCH_REHEARSE") == "1"
-    if rehearse:
-        local = 0
+    rehearse = os.environ.get("FA2_BENCH_REHEARSE") == "1" or args.dry_run
     if world > 1:
-        torch.cuda.set_device(local)
         if rehearse:
             dist.init_process_group("gloo")
         else:
+            torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    B, H, S, D, per_rank = WORKLOADS[args.workload]
     if per_rank:
-        heads = B * H
-        Bl, Hl = B, H
+        heads, Bl, Hl = B * H, B, H
     else:
-        first, heads = fa2amd.shard_range(B * H, world, rank)
-        Bl, Hl = 1, heads
+        import fa2amd
 
+        _, heads = fa2amd.shard_range(B * H, world, rank)
+        Bl, Hl = 1, heads
+    total_heads = B * H * world if per_rank else B * H
+    parallelism = f"bh-shard{world}" if world > 1 else "single"
+    workload_name = f"B{B}_H{H}_S{S}_D{D} {args.precision}-tile fwd+bwd" + (
+        " per rank" if per_rank else (f", B*H split over {world} ranks" if world > 1 else ""))
+
+    if args.dry_run:
+        if world > 1:
+            t = all_max(torch, dist, None, float(rank))
+            dist.barrier()
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "TFLOPS", "n_gpus": world, "dry_run": True,
+                              "scaling": "weak" if per_rank else "strong", "heads_rank0": heads,
+                              "config": {"workload": workload_name, "parallelism": parallelism}}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
+
+    import fa2amd
+
+    local_dev = 0 if rehearse else local
+    dev = torch.device("cuda", local_dev)
+    torch.cuda.set_device(dev)
     gen = torch.Generator().manual_seed(42 + rank)
     q = torch.rand(Bl, Hl, S, D, generator=gen).to(dev)
     k = torch.rand(Bl, Hl, S, D, generator=gen).to(dev)
@@ -265,9 +384,7 @@ def main():
     dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
     stream = torch.cuda.current_stream(dev)
     prec = args.precision
-
-    # fp16: dQ (with Δ fused into its prologue) then dK/dV, as fa2_backward runs them
-    kernels = ["fwd", "dq", "dkdv"] if prec == "fp16" else ["fwd", "bwd"]
+    kernels = ["fwd", "bwd"]
 
     def step(ev=None):
         def mark(i):
@@ -276,14 +393,8 @@ def main():
         mark(0)
         fa2amd.forward(q, k, v, prec, out=o, lse=lse, stream=stream)
         mark(1)
-        if prec == "fp16":
-            fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq, stream=stream)
-            mark(2)
-            fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv, stream=stream)
-            mark(3)
-        else:
-            fa2amd.backward(q, k, v, o, do, lse, prec, dq=dq, dk=dk, dv=dv, delta_buf=dl, stream=stream)
-            mark(2)
+        fa2amd.backward(q, k, v, o, do, lse, prec, dq=dq, dk=dk, dv=dv, delta_buf=dl, stream=stream)
+        mark(2)
 
     # Untimed warmup: at least W steps AND at least --warmup-ms of load.  With 5 warmup
     # steps (~2 ms) the clock is still ramping when the timed region starts and a 20-step
@@ -297,17 +408,15 @@ def main():
         if warm_steps >= args.warmup:
             torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
-    nev = len(kernels) + 1
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(nev)] for _ in range(args.steps)]
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(len(kernels) + 1)] for _ in range(args.steps)]
 
     # timed region 1 -> value: K steps exactly as a caller issues them (no event between
-    # kernels: a timing event serialises the stream, so the next kernel's workgroups
-    # can no longer start on CUs the previous kernel has freed -- ~12 % on the step)
+    # kernels: a timing event serialises the stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for s in range(args.steps):
+    for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -315,9 +424,8 @@ def main():
         dist.barrier()
         elapsed = all_max(torch, dist, dev, elapsed)
 
-    # timed region 2 -> roofline: the same K steps with HIP events around every kernel
-    # on its stream; these per-launch durations are the isolated ones rocprofv3's
-    # kernel trace also reports (it serialises dispatches the same way)
+    # timed region 2 -> roofline: the same K steps with HIP events around every launch
+    # on its stream (the isolated per-launch durations rocprofv3's kernel trace reports)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     for s in range(args.steps):
@@ -328,23 +436,22 @@ def main():
            for i, name in enumerate(kernels)}
 
     per_head = S * S * D
-    total_heads = B * H * world if per_rank else B * H
     flops = 14.0 * per_head * total_heads * args.steps
     tflops = flops / elapsed / 1e12
     hbm_bytes = (48.0 * S * D + 8.0 * S) * total_heads * args.steps  # fwd 16SD+4S, bwd 32SD+4S per head
     ms_per_step = elapsed / args.steps * 1e3
 
-    # dominant kernel and its algorithmic FLOPs per launch
-    alg = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "delta": 0.0, "bwd": 10.0}
+    # dominant launch and its algorithmic FLOPs (fwd 4 S^2 D, bwd 10 S^2 D per head);
+    # at C3 fa2_backward is one launch (the one-pass kernel)
+    alg = {"fwd": 4.0, "bwd": 10.0}
     dom = max(kms, key=kms.get)
     dom_flops = alg[dom] * per_head * heads
     peak = MFMA_F16_PEAK_TFLOPS if prec in ("fp16", "bf16") else MFMA_F32_PEAK_TFLOPS
     achieved = dom_flops / (kms[dom] * 1e-3) / 1e12
+    traffic = traffic_from_profile(dom if prec != "fp32" else "bwd32", D, S, heads)
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic_from_profile(dom, D, S, heads),
+            "frac": round(achieved / peak, 4), "traffic": traffic,
             "kernel_ms": {n: round(x, 4) for n, x in kms.items()},
-            "kernel_ms_note": "isolated per-launch durations (events around every kernel, as rocprofv3 times them); "
-                              "the step without events overlaps kernel boundaries",
             "ms_per_step_with_events": round(elapsed_ev / args.steps * 1e3, 4)}
 
     cpu = None
@@ -355,18 +462,13 @@ def main():
         extra = {f"sweep_B2_H8_D64_fp16_fwdbwd_sharded{world}": sweep_sharded(fa2amd, torch, dev, dist, world, rank)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(S, D)
+            cpu = cpu_baseline(S, D, 16)
         except Exception as e:  # the baseline is reported, never required
             log("cpu baseline failed:", e)
-        try:
-            if cpu is not None:
-                cpu["torch_sdpa_cpu"] = torch_sdpa_cpu(S, D, 16)
-        except Exception as e:
-            log("torch cpu baseline failed:", e)
 
     if rank == 0:
         line = {
-            "metric": "FA2 fwd+bwd TFLOPS & HBM GB/s (% of gfx950 roofline) at S=2048 D=64",
+            "metric": METRIC,
             "value": round(tflops, 3),
             "unit": "TFLOPS",
             "n_gpus": world,
@@ -379,9 +481,8 @@ def main():
             "vs_baseline": None,
             "dtype": prec,
             "data": "synthetic (torch.rand U[0,1) Q/K/V as the reference harness draws them, dO = ones)",
-            "config": {"workload": f"B{B}_H{H}_S{S}_D{D} {prec}-tile fwd+bwd" + (" per rank" if per_rank else ""),
-                       "batch": B, "heads": H, "seq_len": S, "head_dim": D,
-                       "parallelism": f"bh-shard{world}" if world > 1 else "single"},
+            "config": {"workload": workload_name, "batch": B, "heads": H, "seq_len": S, "head_dim": D,
+                       "parallelism": parallelism},
             "hbm_gbps": round(hbm_bytes / elapsed / 1e9, 2),
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -390,7 +491,8 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main())

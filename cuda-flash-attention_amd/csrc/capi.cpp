@@ -358,13 +358,17 @@ int run_shard(HostJob& j) {
 int run_sharded(HostJob proto, int B, int H, int num_devices, float* kernel_ms) {
     const int total = B * H;
     int ndev = num_devices < 1 ? 1 : num_devices;
+    // test-only override HOST_SHARDS_ON_DEVICE0 (fa2_tune_set): every shard runs on
+    // device 0, each on its own thread and stream, so a one-GPU box exercises the
+    // non-zero head offsets of an N-way split
+    const bool one_device = fa2::tune_knob("HOST_SHARDS_ON_DEVICE0", 0) != 0;
     const int avail = fa2_device_count();
-    if (avail < ndev) return fail(FA2_E_INVALID, "num_devices exceeds the visible devices");
+    if (avail < (one_device ? 1 : ndev)) return fail(FA2_E_INVALID, "num_devices exceeds the visible devices");
     if (ndev > total) ndev = total;
     std::vector<HostJob> jobs(ndev, proto);
     for (int g = 0; g < ndev; ++g) {
         fa2_shard_range(total, ndev, g, &jobs[g].heads0, &jobs[g].nheads);
-        jobs[g].device = g;
+        jobs[g].device = one_device ? 0 : g;
     }
     auto body = [](HostJob* j) {
         j->rc = run_shard(*j);

@@ -75,3 +75,26 @@ def test_bench_shard_covers_all_heads(total, world):
         sizes.append(c)
     assert seen == list(range(total))
     assert max(sizes) - min(sizes) <= 1
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`python bench.py --gpus 2` with no launcher starts two ranks itself (before any
+    GPU call) on the north star's C5 strong-scaling split; --dry-run keeps it to the
+    rank plumbing (gloo barrier + max over ranks), so it runs on CPU."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2
+    assert line["config"]["parallelism"] == "bh-shard2"
+    assert line["scaling"] == "strong"
+    assert line["config"]["workload"].startswith("B64_H16_S2048_D64")
+    assert line["heads_rank0"] == 512
