@@ -11,6 +11,13 @@ Mirrors the reporting side of test_flash_attention2.py (detker/CUDA-Flash-Attent
   kernel-comparison plots (:1126-1287; matplotlib only, the reference's seaborn
   styling is not installed here).
 
+Modes (``--mode``, :1466-1469): ``forward``; ``backward`` (the FA2 backward fed
+with the PyTorch forward's O and LSE, as the harness does, :898-925); ``both``
+(the FA2 forward, then the FA2 backward on the forward's own O and LSE, metrics
+summed as in ``_run_test_both``, :608-794).  ``--no-stop-on-failure`` (:1482)
+keeps going after a failing row (the default stops, :1091-1095);
+``--no-gpu-reference`` (:1488) drops the PyTorch GPU rows.
+
 Kernels: ``fa2`` (the C ABI, precision fp32 / fp16 / bf16), ``fa1``, ``vanilla-attn``
 (the comparison baselines, fp32 forward, C ABI) and ``fa2-naive`` (kernels/plain-attn.cu
 through its CuPy face, head_dim 64).  Expected values are the
@@ -118,7 +125,7 @@ def _gpu_time(fn, runs=10):
 _BASELINE = None  # hiprtc-compiled baseline modules, built on first use
 
 
-def run_forward(name, B, H, S, D, kernels, precision="fp32", tolerance=1e-3):
+def run_forward(name, B, H, S, D, kernels, precision="fp32", tolerance=1e-3, gpu_reference=True):
     import torch
 
     import fa2amd
@@ -131,10 +138,11 @@ def run_forward(name, B, H, S, D, kernels, precision="fp32", tolerance=1e-3):
                 {**harness.compute_metrics(exp, exp, torch_ms, torch_ms, B, H, S, D), "speedup": 1.0},
                 torch_ms, torch_ms)]
     tq, tk, tv = (x.cuda() for x in (q, k, v))
-    gpu_ms = _gpu_time(lambda: torch.nn.functional.scaled_dot_product_attention(tq, tk, tv))
-    og = torch.nn.functional.scaled_dot_product_attention(tq, tk, tv).cpu().numpy()
-    rows.append(Row(name, "pytorch gpu", "forward", B, H, S, D, True,
-                    harness.compute_metrics(og, exp, gpu_ms, torch_ms, B, H, S, D), gpu_ms, torch_ms))
+    if gpu_reference:
+        gpu_ms = _gpu_time(lambda: torch.nn.functional.scaled_dot_product_attention(tq, tk, tv))
+        og = torch.nn.functional.scaled_dot_product_attention(tq, tk, tv).cpu().numpy()
+        rows.append(Row(name, "pytorch gpu", "forward", B, H, S, D, True,
+                        harness.compute_metrics(og, exp, gpu_ms, torch_ms, B, H, S, D), gpu_ms, torch_ms))
     for kern in kernels:
         try:
             if kern == "fa2":
@@ -167,22 +175,129 @@ def run_forward(name, B, H, S, D, kernels, precision="fp32", tolerance=1e-3):
     return rows
 
 
-def run_backward(name, B, H, S, D, precision="fp32", tolerance=1e-3):
+def _gpu_reference_grads(q, k, v):
+    """PyTorch GPU SDPA forward + autograd backward (dO = ones), one warm-up, one timed
+    run (the harness's GPU reference rows, :836-880 and :651-699)."""
+    import torch
+
+    def once():
+        qq, kk, vv = (x.detach().cuda().requires_grad_() for x in (q, k, v))
+        o = torch.nn.functional.scaled_dot_product_attention(qq, kk, vv)
+        o.backward(torch.ones_like(o))
+        return o, qq.grad, kk.grad, vv.grad
+
+    once()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    o, dq, dk, dv = once()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    return o.detach().cpu().numpy(), [g.cpu().numpy() for g in (dq, dk, dv)], ms
+
+
+def _bwd_metrics(harness, got, exp, ms, torch_ms, B, H, S, D):
+    met = harness.compute_metrics(got, exp, ms, torch_ms, B, H, S, D)
+    met["tflops"] = 2.5 * 4 * B * H * S * S * D / (ms * 1e-3) / 1e12 if ms > 0 else 0.0  # :634
+    return met
+
+
+def run_backward(name, B, H, S, D, precision="fp32", tolerance=1e-3, gpu_reference=True):
+    """--mode backward (:812-940): the FA2 backward is fed the PyTorch forward's O and
+    its LSE (natural log, max-shifted, :905-921), as the harness does; dO = ones."""
+    import torch
+
     import fa2amd
     from . import harness
 
     q, k, v = harness_inputs(B, H, S, D)
     o_ref, grads_ref, torch_ms = torch_reference_backward(q, k, v)
     exp = np.concatenate([g.numpy().ravel() for g in grads_ref])
+    cpu_met = _bwd_metrics(harness, exp, exp, torch_ms, torch_ms, B, H, S, D)
+    rows = [Row(name, "pytorch cpu", "backward", B, H, S, D, True, {**cpu_met, "speedup": 1.0}, torch_ms, torch_ms)]
+    if gpu_reference:
+        _, gg, gms = _gpu_reference_grads(q, k, v)
+        got = np.concatenate([g.ravel() for g in gg])
+        rows.append(Row(name, "pytorch gpu", "backward", B, H, S, D, True,
+                        _bwd_metrics(harness, got, exp, gms, torch_ms, B, H, S, D), gms, torch_ms))
+    s = torch.matmul(q, k.transpose(-2, -1)) / np.sqrt(D)
+    m = s.max(dim=-1, keepdim=True)[0]
+    lse = (m.squeeze(-1) + torch.log(torch.exp(s - m).sum(dim=-1))).numpy()
     r = harness.FA2Runner(precision)
-    out, lse, _ = r.run_fa2_forward_kernel(q, k, v)
-    grads, ms = r.run_cuda_fa2_backward_kernel(q, k, v, out, np.ones_like(out), lse)
-    got = np.concatenate([grads[n].ravel() for n in ("dQ", "dK", "dV")])
-    met = harness.compute_metrics(got, exp, ms, torch_ms, B, H, S, D)
-    flops = 2.5 * 4 * B * H * S * S * D  # the harness's backward accounting (:634)
-    met["tflops"] = flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     label = "fa2" if precision == "fp32" else f"fa2-{precision}"
-    return [Row(name, label, "backward", B, H, S, D, harness.passed(met, got, tolerance), met, ms, torch_ms)]
+    try:
+        grads, ms = r.run_cuda_fa2_backward_kernel(q, k, v, o_ref.numpy(), np.ones(q.shape, np.float32), lse)
+        got = np.concatenate([grads[n].ravel() for n in ("dQ", "dK", "dV")])
+        met = _bwd_metrics(harness, got, exp, ms, torch_ms, B, H, S, D)
+        rows.append(Row(name, label, "backward", B, H, S, D, harness.passed(met, got, tolerance), met, ms, torch_ms))
+    except Exception as e:  # a FAIL row, as the harness records errors
+        rows.append(Row(name, label, "backward", B, H, S, D, False, {}, 0.0, torch_ms, str(e)))
+    return rows
+
+
+def run_both(name, B, H, S, D, precision="fp32", tolerance=1e-3, gpu_reference=True):
+    """--mode both (_run_test_both, :608-794): the FA2 forward, then the FA2 backward on
+    the forward's own O and LSE.  One row per implementation; the FA2 row passes when
+    both the output and the concatenated gradients pass the harness rule, its time is
+    forward + backward, TFLOPS counts 3.5x the forward FLOPs (:633-635), bandwidth is
+    the sum of the two passes' (:766)."""
+    import fa2amd  # noqa: F401  (the C ABI must load)
+    from . import harness
+
+    q, k, v = harness_inputs(B, H, S, D)
+    o_exp, fwd_ms = torch_reference(q, k, v)
+    _, grads_ref, bwd_ms = torch_reference_backward(q, k, v)
+    torch_ms = fwd_ms + bwd_ms
+    o_exp = o_exp.numpy()
+    exp = np.concatenate([g.numpy().ravel() for g in grads_ref])
+    total_flops = 3.5 * 4 * B * H * S * S * D
+    bytes_ = B * H * S * D * 4 * 4
+
+    def rates(ms):
+        return (total_flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0,
+                bytes_ / (ms * 1e-3) / 1e9 if ms > 0 else 0.0)
+
+    tf, bw = rates(torch_ms)
+    rows = [Row(name, "pytorch cpu", "both", B, H, S, D, True,
+                {"max_abs_error": 0.0, "mean_abs_error": 0.0, "mse": 0.0, "max_rel_error": 0.0, "speedup": 1.0,
+                 "tflops": tf, "bandwidth_gbps": bw}, torch_ms, torch_ms)]
+    if gpu_reference:
+        og, gg, gms = _gpu_reference_grads(q, k, v)
+        got = np.concatenate([g.ravel() for g in gg])
+        fe, be = np.abs(og - o_exp), np.abs(got - exp)
+        tf, bw = rates(gms)
+        rows.append(Row(name, "pytorch gpu", "both", B, H, S, D, True,
+                        {"max_abs_error": float(max(fe.max(), be.max())),
+                         "mean_abs_error": float((fe.mean() + be.mean()) / 2), "mse": 0.0, "max_rel_error": 0.0,
+                         "speedup": torch_ms / gms if gms > 0 else 0.0, "tflops": tf, "bandwidth_gbps": bw},
+                        gms, torch_ms))
+    label = "fa2" if precision == "fp32" else f"fa2-{precision}"
+    try:
+        r = harness.FA2Runner(precision)
+        out, lse, f_ms = r.run_fa2_forward_kernel(q, k, v)
+        fm = harness.compute_metrics(out, o_exp, f_ms, fwd_ms, B, H, S, D)
+        fwd_ok = harness.passed(fm, out, tolerance)
+        grads, b_ms = r.run_cuda_fa2_backward_kernel(q, k, v, out, np.ones(q.shape, np.float32), lse)
+        got = np.concatenate([grads[n].ravel() for n in ("dQ", "dK", "dV")])
+        bm = harness.compute_metrics(got, exp, b_ms, bwd_ms, B, H, S, D)
+        bwd_ok = harness.passed(bm, got, tolerance)
+        ms = f_ms + b_ms
+        tf, _ = rates(ms)
+        met = {"max_abs_error": max(fm["max_abs_error"], bm["max_abs_error"]),
+               "mean_abs_error": (fm["mean_abs_error"] + bm["mean_abs_error"]) / 2,
+               "mse": (fm["mse"] + bm["mse"]) / 2, "max_rel_error": max(fm["max_rel_error"], bm["max_rel_error"]),
+               "speedup": torch_ms / ms if ms > 0 else 0.0, "tflops": tf,
+               "bandwidth_gbps": fm["bandwidth_gbps"] + bm["bandwidth_gbps"],
+               "fwd_max_abs_error": fm["max_abs_error"], "bwd_max_abs_error": bm["max_abs_error"],
+               "fwd_ms": f_ms, "bwd_ms": b_ms}
+        err = ""
+        if not fwd_ok:
+            err += f"Forward failed (err={fm['max_abs_error']:.2e}). "
+        if not bwd_ok:
+            err += f"Backward failed (err={bm['max_abs_error']:.2e}). "
+        rows.append(Row(name, label, "both", B, H, S, D, fwd_ok and bwd_ok, met, ms, torch_ms, err.strip()))
+    except Exception as e:
+        rows.append(Row(name, label, "both", B, H, S, D, False, {}, 0.0, torch_ms, str(e)))
+    return rows
 
 
 def write_csv(rows, path):
@@ -226,19 +341,28 @@ def plot(rows, out_dir):
     return path
 
 
+CSV_NAME = {"forward": "experiment_results.csv", "backward": "backward_experiment_results.csv",
+            "both": "both_experiment_results.csv"}
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
-    ap.add_argument("--mode", choices=["forward", "backward"], default="forward")
+    ap.add_argument("--mode", choices=["forward", "backward", "both"], default="forward")
     ap.add_argument("--kernel", choices=["fa2", "fa1", "vanilla-attn", "fa2-naive"], default="fa2")
     ap.add_argument("--precision", choices=["fp32", "fp16", "bf16"], default="fp32")
     ap.add_argument("--experiment", action="store_true", help="every kernel on every test config")
     ap.add_argument("--seqlen-experiment", action="store_true", help="B4_H8_D64, S = 128..4096")
     ap.add_argument("--tolerance", type=float, default=1e-3)
+    ap.add_argument("--no-stop-on-failure", action="store_true", help="continue testing after the first failure")
+    ap.add_argument("--no-gpu-reference", action="store_true", help="no PyTorch GPU reference rows")
     ap.add_argument("--configs", default="", help="comma-separated subset of config names")
     ap.add_argument("--save-results", action="store_true")
     ap.add_argument("--output-dir", default="./experiment_results")
     args = ap.parse_args(argv)
 
+    # :1494-1495 -- only fa2 has a backward
+    if args.mode in ("backward", "both") and args.kernel != "fa2":
+        ap.error(f"Only 'fa2' kernel supports backward pass. Got --kernel={args.kernel} with --mode={args.mode}")
     if args.seqlen_experiment:
         configs = [(f"SeqLen-S{s}", 4, 8, s, 64) for s in SEQLEN_SWEEP]
     else:
@@ -246,24 +370,30 @@ def main(argv=None):
     if args.configs:
         keep = set(args.configs.split(","))
         configs = [c for c in configs if c[0] in keep]
-    kernels = FORWARD_KERNELS if (args.experiment or args.seqlen_experiment) else (args.kernel,)
-    if args.mode == "backward" and kernels != ("fa2",) and not args.experiment:
-        ap.error(f"Only 'fa2' kernel supports backward pass. Got --kernel={args.kernel}")  # :1494-1495
+    forward_set = args.mode == "forward" and (args.experiment or args.seqlen_experiment)
+    kernels = FORWARD_KERNELS if forward_set else (args.kernel,)
+    gpu_ref = not args.no_gpu_reference
+    stop = not args.no_stop_on_failure
 
     rows = []
     for name, B, H, S, D in configs:
         if args.mode == "forward":
-            rows += run_forward(name, B, H, S, D, kernels, args.precision, args.tolerance)
+            new = run_forward(name, B, H, S, D, kernels, args.precision, args.tolerance, gpu_ref)
+        elif args.mode == "backward":
+            new = run_backward(name, B, H, S, D, args.precision, args.tolerance, gpu_ref)
         else:
-            rows += run_backward(name, B, H, S, D, args.precision, args.tolerance)
-        for r in rows[-(len(kernels) + 2 if args.mode == "forward" else 1):]:
+            new = run_both(name, B, H, S, D, args.precision, args.tolerance, gpu_ref)
+        rows += new
+        for r in new:
             print(f"{r.test:18s} {r.kernel.upper():14s} {r.type[:3].upper()} {'PASS' if r.passed else 'FAIL'} "
                   f"max_err {r.metrics.get('max_abs_error', float('nan')):.3e} {r.kernel_ms:9.4f} ms "
                   f"{r.metrics.get('tflops', 0.0):8.3f} TFLOPS {r.error}", flush=True)
+        if stop and not all(r.passed for r in new):
+            print("Stopping on first failure (stop_on_failure=True)", flush=True)  # :1091-1095
+            break
     if args.save_results:
         os.makedirs(args.output_dir, exist_ok=True)
-        name = "experiment_results.csv" if args.mode == "forward" else "backward_experiment_results.csv"
-        write_csv(rows, os.path.join(args.output_dir, name))
+        write_csv(rows, os.path.join(args.output_dir, CSV_NAME[args.mode]))
         plot(rows, args.output_dir)
     return 0 if all(r.passed for r in rows) else 1
 

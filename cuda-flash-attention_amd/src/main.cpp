@@ -26,11 +26,6 @@ int main(int argc, char** argv) {
     parse_config_string(data_path, &B, &H, &S, &D);
     check_method_support(method, mode, precision);
 
-    // (argv is validated before the device timer is created, so a bad command
-    // line fails the same way on a host without a GPU)
-    TimerManager tm;
-    TimerGPU timer_gpu;
-    tm.SetTimer(&timer_gpu);
     const size_t n = (size_t)B * H * S * D;
     const size_t nl = (size_t)B * H * S;
     printf("Batch size:    %d\n", B);
@@ -69,6 +64,11 @@ int main(int argc, char** argv) {
     }
     printf("Data loaded successfully.\n\n");
 
+    // (argv and the input files are checked before the device timer is created, so
+    // a bad command line or a missing/short file fails the same way without a GPU)
+    TimerManager tm;
+    TimerGPU timer_gpu;
+    tm.SetTimer(&timer_gpu);
     printf("Running...\n");
     RunFlashAttention(q.data(), k.data(), v.data(), o.data(), lse.data(), bwd ? dout.data() : nullptr,
                       bwd ? dq.data() : nullptr, bwd ? dk.data() : nullptr, bwd ? dv.data() : nullptr, B, H, S, D,

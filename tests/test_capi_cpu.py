@@ -183,3 +183,44 @@ def test_experiment_csv_columns(tmp_path):
     assert lines[0].split(",") == experiments.CSV_COLUMNS
     assert lines[1].startswith("Small-1,FA2,FOR,1,1,128,64,PASS,")
     assert lines[2].startswith("Small-1,FA1,FOR,1,1,128,64,FAIL,") and lines[2].endswith("boom")
+
+
+def test_experiment_cli_flags(monkeypatch, tmp_path):
+    """The harness's --mode both / --no-stop-on-failure / --no-gpu-reference
+    (test_flash_attention2.py:1466-1495) and its stop-on-first-failure loop
+    (:1091-1095), with the per-config runners stubbed (no GPU here)."""
+    from fa2amd import experiments
+
+    with pytest.raises(SystemExit) as e:
+        experiments.main(["--mode", "both", "--kernel", "fa1"])
+    assert e.value.code == 2
+    with pytest.raises(SystemExit):
+        experiments.main(["--mode", "backward", "--kernel", "vanilla-attn"])
+    calls = []
+
+    def fake(mode):
+        def run(name, B, H, S, D, *a):
+            gpu_ref = a[-1]
+            calls.append((mode, name, gpu_ref))
+            ok = name != "Small-2"
+            return [experiments.Row(name, "fa2", mode, B, H, S, D, ok, {"max_abs_error": 0.0 if ok else 1.0},
+                                    0.1, 1.0)]
+        return run
+
+    monkeypatch.setattr(experiments, "run_both", fake("both"))
+    monkeypatch.setattr(experiments, "run_backward", fake("backward"))
+    monkeypatch.setattr(experiments, "run_forward", fake("forward"))
+    cfg = ["--configs", "Small-1,Small-2,Small-3"]
+    assert experiments.main(["--mode", "both"] + cfg) == 1
+    assert [c[1] for c in calls] == ["Small-1", "Small-2"]  # stopped at the first failure
+    assert all(c[2] is True for c in calls)
+    calls.clear()
+    assert experiments.main(["--mode", "both", "--no-stop-on-failure", "--no-gpu-reference", "--save-results",
+                             "--output-dir", str(tmp_path)] + cfg) == 1
+    assert [c[1] for c in calls] == ["Small-1", "Small-2", "Small-3"]
+    assert all(c[2] is False for c in calls)
+    lines = (tmp_path / "both_experiment_results.csv").read_text().splitlines()
+    assert [ln.split(",")[2] for ln in lines[1:]] == ["BOT"] * 3
+    calls.clear()
+    assert experiments.main(["--mode", "backward", "--configs", "Small-1"]) == 0
+    assert calls == [("backward", "Small-1", True)]

@@ -144,3 +144,35 @@ def test_experiment_run_writes_harness_csv(tmp_path):
                            "--save-results", "--output-dir", str(tmp_path)])
     assert rc == 0
     assert (tmp_path / "backward_experiment_results.csv").exists()
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-3), ("fp16", 1e-2)])
+def test_experiment_mode_both(tmp_path, precision, tol):
+    """--mode both (_run_test_both, test_flash_attention2.py:608-794): the FA2 forward,
+    then the FA2 backward on its own O and LSE; the FA2 row passes the harness rule on
+    the output AND the concatenated gradients; CPU and GPU reference rows beside it."""
+    from fa2amd import experiments
+
+    rows = experiments.run_both("Edge-NonPowerOf2", 2, 4, 100, 64, precision, tol)
+    kinds = [r.kernel for r in rows]
+    assert kinds[:2] == ["pytorch cpu", "pytorch gpu"] and kinds[2].startswith("fa2")
+    fa2 = rows[2]
+    assert fa2.passed, fa2.error
+    assert fa2.metrics["fwd_max_abs_error"] < tol and fa2.metrics["bwd_max_abs_error"] < tol
+    assert fa2.kernel_ms == pytest.approx(fa2.metrics["fwd_ms"] + fa2.metrics["bwd_ms"])
+    rc = experiments.main(["--mode", "both", "--configs", "Small-1,Edge-SmallSeq", "--precision", precision,
+                           "--tolerance", str(tol), "--no-gpu-reference", "--save-results", "--output-dir",
+                           str(tmp_path)])
+    assert rc == 0
+    lines = (tmp_path / "both_experiment_results.csv").read_text().splitlines()[1:]
+    assert len(lines) == 4 and all(",BOT," in ln and ",PASS," in ln for ln in lines)
+    assert not any("PYTORCH GPU" in ln for ln in lines)
+
+
+def test_experiment_mode_backward_uses_torch_forward():
+    """--mode backward feeds the FA2 backward the PyTorch forward's O and LSE (:898-925)."""
+    from fa2amd import experiments
+
+    rows = experiments.run_backward("Small-2", 2, 4, 256, 64, "fp32", 1e-3, gpu_reference=False)
+    assert [r.kernel for r in rows] == ["pytorch cpu", "fa2"]
+    assert rows[1].passed, rows[1].error
