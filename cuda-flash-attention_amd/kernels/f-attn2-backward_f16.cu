@@ -238,7 +238,8 @@ struct TileStager {
 // its dO and O stagers: the CPR threads that hold one row's chunks are consecutive
 // lanes, reduced with xor shuffles.  Δ goes to `delta_lds` (this workgroup's rows)
 // and to HBM for the dK/dV kernel.
-template <int D, int ROWS, int NT>
+// NEG: -Δ into `delta_lds` (the dP accumulators' initial value); delta_out may be null.
+template <int D, int ROWS, int NT, bool NEG = false>
 __device__ __forceinline__ void delta_rows(const TileStager<D, ROWS, NT>& a, const TileStager<D, ROWS, NT>& o, int S,
                                            int row0, float* delta_lds, float* __restrict__ delta_out, int tid) {
     using TS = TileStager<D, ROWS, NT>;
@@ -251,8 +252,8 @@ __device__ __forceinline__ void delta_rows(const TileStager<D, ROWS, NT>& a, con
         for (int off = TS::CPR / 2; off > 0; off >>= 1) d += __shfl_xor(d, off);
         const int row = x / TS::CPR;
         if ((TS::EXACT || x < TS::CHUNKS) && x % TS::CPR == 0) {
-            delta_lds[row] = d;
-            if (row0 + row < S) delta_out[row0 + row] = d;
+            delta_lds[row] = NEG ? -d : d;
+            if (delta_out && row0 + row < S) delta_out[row0 + row] = d;
         }
     }
 }
@@ -521,12 +522,14 @@ struct DkdvLds {
 
 // One workgroup of the dK/dV kernel; `bid` is its (XCD-remapped) block number over
 // the BH * ceil(S / (KPW * NK)) key blocks.
-template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1>
+// DEL: Δ = rowsum(dO ∘ O) of every staged step computed here from O rows staged
+// beside dO (no Delta input: the fused small-grid launch, whose dQ role writes Δ).
+template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1, bool DEL = false>
 __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const float* __restrict__ Q,
                                           const float* __restrict__ K, const float* __restrict__ V,
                                           const float* __restrict__ dO, const float* __restrict__ LSE,
                                           const float* __restrict__ Delta, float* __restrict__ dK,
-                                          float* __restrict__ dV, int S) {
+                                          float* __restrict__ dV, int S, const float* __restrict__ O = nullptr) {
     using L = DkdvLds<D, NW, KB, QS>;
     constexpr int QT = L::QT;  // query rows per step
     constexpr int NT = 64 * NW;
@@ -626,14 +629,16 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
                 }
     }
 
-    // next-step staging by the first SW waves (FA2_DKDV_SW, above)
-    constexpr int SW = FA2_DKDV_SW < NW ? FA2_DKDV_SW : NW;
+    // next-step staging by the first SW waves (FA2_DKDV_SW, above); DEL stages O too,
+    // by every wave (at 8 waves x QS = 2 the 4-wave staging registers spilled ~290 VGPRs)
+    constexpr int SW = DEL ? NW : FA2_DKDV_SW < NW ? FA2_DKDV_SW : NW;
     constexpr int NS = 64 * SW;
     const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool stg = wave_u < SW;
-    TileStager<D, QT * QS, NS> qs, dos;
+    TileStager<D, QT * QS, NS> qs, dos, os;
     qs.init(Q + base, S, tid);
     dos.init(dO + base, S, tid);
+    if constexpr (DEL) os.init(O + base, S, tid);
     // Row constants of the staged step: wave 0 carries LSE, wave 1 carries Delta
     // (QT == 64 == one wave).  Loaded raw by a range-checked buffer load (rows >= S
     // read 0) and only scaled / negated / masked at store time, so nothing waits on
@@ -651,12 +656,13 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         q0 += rw * QT;
         rowq = q0 + lane;
         if (wave_u < QS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
-        else if (wave_u < 2 * QS) rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_del, lane * 4, q0 * 4, 0));
+        else if (!DEL && wave_u < 2 * QS)
+            rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_del, lane * 4, q0 * 4, 0));
     };
     auto store_rows = [&](int buf) {
         // stored negated: they are the initial accumulators of S and dP
         if (wave_u < QS) rows[buf][0][rw * QT + lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
-        else if (wave_u < 2 * QS) rows[buf][1][rw * QT + lane] = -rowraw;
+        else if (!DEL && wave_u < 2 * QS) rows[buf][1][rw * QT + lane] = -rowraw;
     };
     // the next step's global loads go out between the step's two query blocks (issued
     // all at once right after the barrier they queue on the texture unit: r01)
@@ -664,6 +670,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         if (stg) {
             qs.load(it * QS * QT);
             dos.load(it * QS * QT);
+            if constexpr (DEL) os.load(it * QS * QT);
         }
         load_rows(it * QS * QT);
     };
@@ -671,6 +678,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         if (stg) {
             qs.store(qdst, 1.f, tid);
             dos.store(ddst, 1.f, tid);
+            if constexpr (DEL) delta_rows<D, QT * QS, NS, true>(dos, os, S, 0, rows[rbuf][1], nullptr, tid);
         }
         store_rows(rbuf);
     };
@@ -679,6 +687,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
     if (stg) {
         qs.load(0);
         dos.load(0);
+        if constexpr (DEL) os.load(0);
     }
     load_rows(0);
     if constexpr (L::OVL) {
@@ -1166,19 +1175,25 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 // prior fa2_delta_kernel (the dQ role cannot hand its fused Δ to the dK/dV role
 // without a cross-workgroup wait).  Both roles run NW waves on the 16x16x32 path;
 // the LDS block is the larger of the two layouts, registers the larger of the two.
-template <int D, int NW, int QS, int KS, int NKB>
+//   DEL (O given): no Δ input at all.  Each role computes Δ = rowsum(dO ∘ O) from O rows
+// staged beside the dO rows it stages anyway -- the dQ role in its prologue (and it
+// writes Δ out), the dK/dV role per step -- so the launch depends on nothing but the
+// forward's outputs: the separate Δ kernel and its launch boundary go away, at the
+// price of the dK/dV role's O reads (these grids are latency-bound, not HBM-bound).
+template <int D, int NW, int QS, int KS, int NKB, bool DEL = false>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                         const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-                         float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV, int S, int ndk) {
-    constexpr int B1 = DkdvLds<D, NW, 1, QS>::BYTES, B2 = DqLds<D, NW, false, NKB, KS>::BYTES;
+                         const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
+                         float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV, int S, int ndk,
+                         const float* __restrict__ O) {
+    constexpr int B1 = DkdvLds<D, NW, 1, QS>::BYTES, B2 = DqLds<D, NW, DEL, NKB, KS>::BYTES;
     __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
     const int b = blockIdx.x;
     if (b < ndk)
-        dkdv_body<D, NW, 1, true, QS>(lds, xcd_remap(b, ndk), Q, K, V, dO, LSE, Delta, dK, dV, S);
+        dkdv_body<D, NW, 1, true, QS, DEL>(lds, xcd_remap(b, ndk), Q, K, V, dO, LSE, Delta, dK, dV, S, O);
     else
-        dq_body<D, NW, false, NKB, true, KS>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
-                                             const_cast<float*>(Delta), dQ, S, nullptr);
+        dq_body<D, NW, DEL, NKB, true, KS>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE, Delta, dQ, S,
+                                           O);
 }
 
 // ===========================================================================
@@ -1225,9 +1240,6 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
 // head's other key blocks read the same rows from L2); key block 0 writes it out.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) unsigned gu32;
-#ifndef FA2_OP_ABL
-#define FA2_OP_ABL 0  // TEMPORARY timing ablations
-#endif
 
 // workspace words (u32): [0, 8) per-XCD queue heads, then these; flags from OP_WS_FLAGS
 enum { OP_WS_EXITED = 8, OP_WS_EPOCH = 9, OP_WS_ABORT = 10, OP_WS_FLAGS = 16 };
@@ -1355,7 +1367,6 @@ __device__ __forceinline__ void op_step(DkdvState16<D>& st, const _Float16* Qs, 
             }
         // dS into the dSᵀ image: k-slots 0..3 are queries qb*32 + 4g + 0..3, 4..7 are
         // qb*32 + 16 + 4g + 0..3, of key row 16 nb + (l & 15)
-        if (!(FA2_OP_ABL & 8))
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
             const i16x8 v = __builtin_bit_cast(i16x8, dsf[nb]);
@@ -1384,7 +1395,6 @@ __device__ __forceinline__ void op_dq(f32x4 (&acc)[D / 32], const _Float16* kimg
                                       const OpOffsets<D>& oo) {
 #pragma unroll
     for (int m = 0; m < D / 32; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (!(FA2_OP_ABL & 2)) {
 #pragma unroll
     for (int kk = 0; kk < OP_KEYS / 32; ++kk) {
         const f16x8 b = cat4(lds_tr4(dsimg + oo.db[0] + kk * 32 * 64), lds_tr4(dsimg + oo.db[1] + kk * 32 * 64));
@@ -1392,7 +1402,6 @@ __device__ __forceinline__ void op_dq(f32x4 (&acc)[D / 32], const _Float16* kimg
         for (int m = 0; m < D / 32; ++m)
             acc[m] = mfma16(cat4(lds_tr4(kimg + oo.ka[m][0] + kk * 32 * D), lds_tr4(kimg + oo.ka[m][1] + kk * 32 * D)),
                             b, acc[m]);
-    }
     }
 #pragma unroll
     for (int m = 0; m < D / 32; ++m) acc[m] *= 0.6931471805599453f;
@@ -1438,7 +1447,7 @@ fa2_bwd_onepass_f16_kernel(const float* __restrict__ Q, const float* __restrict_
     int* const slot = reinterpret_cast<int*>(lds + L::MISC);
     float(*ostage)[32][36] = reinterpret_cast<float(*)[32][36]>(lds + 2 * L::DSI);  // epilogue: over the dS images
 
-    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i16 = lane & 15;
+    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nkb = (S + OP_KEYS - 1) / OP_KEYS, nqs = (S + QT - 1) / QT;
     const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
@@ -1497,7 +1506,7 @@ fa2_bwd_onepass_f16_kernel(const float* __restrict__ Q, const float* __restrict_
         auto load_step = [&](int q0) {
             qs.load(q0);
             dos.load(q0);
-            if (!(FA2_OP_ABL & 4)) os.load(q0);
+            os.load(q0);
             if (wave == 0) {
                 rowq = q0 + lane;
                 rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
@@ -1564,7 +1573,7 @@ fa2_bwd_onepass_f16_kernel(const float* __restrict__ Q, const float* __restrict_
                 for (int m = 0; m < MD; ++m) part[m] += sum[m];
             }
             const int soff = hq * QT * D * 4;
-            if ((FA2_OP_ABL & 1) || hpos == nkb - 1) {
+            if (hpos == nkb - 1) {
 #pragma unroll
                 for (int m = 0; m < MD; ++m)
                     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, part[m]), rs_dq, oo.voff[m], soff, 0);
@@ -1601,10 +1610,10 @@ fa2_bwd_onepass_f16_kernel(const float* __restrict__ Q, const float* __restrict_
             const int q1 = more ? qstep(t + 1) * QT : 0;
             const int qt = qstep(t);
             const int hq = t >= 1 ? qstep(t - 1) : 0, hpos = hpos_n;
-            if (t >= 1 && hpos > 0 && !(FA2_OP_ABL & 1)) fetch(hq, hpos, fv_n);
+            if (t >= 1 && hpos > 0) fetch(hq, hpos, fv_n);
             hpos_n = cpos(qt);
             unsigned fv = 0;
-            if (hpos_n > 0 && !(FA2_OP_ABL & 1)) fv = op_ld(flags + qt * 8);
+            if (hpos_n > 0) fv = op_ld(flags + qt * 8);
             op_step<D>(st, smem + 2 * b * TILE, smem + (2 * b + 1) * TILE, rows[b][0], rows[b][1], fo, oo,
                        dsimg + b * L::DSIMG, g, kmask, wkey0, S, [&] {
                            if (more) load_step(q1);
@@ -1632,7 +1641,7 @@ fa2_bwd_onepass_f16_kernel(const float* __restrict__ Q, const float* __restrict_
         // tail: the last step's hop (its part from the last dS image), the dK / dV epilogue
         {
             const int hq = qstep(nqs - 1), hpos = hpos_n;
-            if (hpos > 0 && !(FA2_OP_ABL & 1)) fetch(hq, hpos, fv_n);
+            if (hpos > 0) fetch(hq, hpos, fv_n);
             if ((nqs - 1) & 1) op_dq<D>(part, kimg, dsimg + L::DSIMG, oo);
             else op_dq<D>(part, kimg, dsimg, oo);
             __syncthreads();  // every wave's dQ reads are done: the dS images take the stage
@@ -1973,14 +1982,20 @@ hipError_t FA2_TILE_LAUNCH(launch_bwd_dq_delta)(int D, const float* q, const flo
 }
 
 namespace {
+// o != nullptr: the DEL instance (Δ computed in both roles from O and written to delta)
 template <int D, int NW, int QS, int KS, int NKB>
 hipError_t fused_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
-                        const float* delta, float* dq, float* dk, float* dv, int bh, int S, hipStream_t stream) {
+                        float* delta, float* dq, float* dk, float* dv, int bh, int S, const float* o,
+                        hipStream_t stream) {
     const long ndk = (long)bh * ((S + 32 * (NW / QS) - 1) / (32 * (NW / QS)));
     const long ndq = (long)bh * ((S + 32 * (NW / KS) - 1) / (32 * (NW / KS)));
     if (ndk <= 0 || ndq <= 0 || ndk + ndq > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16b::fa2_bwd_fused_f16_kernel<D, NW, QS, KS, NKB>), dim3((unsigned)(ndk + ndq)),
-                       dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, dk, dv, S, (int)ndk);
+    if (o)
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_fused_f16_kernel<D, NW, QS, KS, NKB, true>), dim3((unsigned)(ndk + ndq)),
+                           dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, dk, dv, S, (int)ndk, o);
+    else
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_fused_f16_kernel<D, NW, QS, KS, NKB>), dim3((unsigned)(ndk + ndq)),
+                           dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, dk, dv, S, (int)ndk, o);
     return hipGetLastError();
 }
 // The fused dK/dV + dQ launch for D <= 64, or hipErrorNotSupported (then the caller
@@ -1989,7 +2004,8 @@ hipError_t fused_launch(const float* q, const float* k, const float* v, const fl
 // KS = 2, else unsplit.  Overrides (fa2_tune_set): BWD_FQS, BWD_FKS, BWD_FNW.
 template <int D>
 hipError_t fused_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
-                          const float* delta, float* dq, float* dk, float* dv, int bh, int S, hipStream_t stream) {
+                          float* delta, float* dq, float* dk, float* dv, int bh, int S, const float* o,
+                          hipStream_t stream) {
     if constexpr (D > 64) {
         return hipErrorNotSupported;
     } else {
@@ -2002,15 +2018,15 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
         const int fks = tune_knob("BWD_FKS", a == 8 ? 1 : (a == 4 || tiny) ? 2 : 4);
         // waves per workgroup of both roles (8, or 4 for the split pairs)
         const int fnw = tune_knob("BWD_FNW", tiny ? 4 : 8);
-        if (fqs == 1 && fks == 1) return fused_launch<D, 8, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        if (fqs == 1 && fks == 1) return fused_launch<D, 8, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
         if (fnw == 4) {
             if (fqs == 2 && fks == 2)
-                return fused_launch<D, 4, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+                return fused_launch<D, 4, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
             if (fqs == 2 && fks == 4)
-                return fused_launch<D, 4, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+                return fused_launch<D, 4, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
         }
-        if (fqs == 2 && fks == 2) return fused_launch<D, 8, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
-        if (fqs == 2 && fks == 4) return fused_launch<D, 8, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        if (fqs == 2 && fks == 2) return fused_launch<D, 8, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
+        if (fqs == 2 && fks == 4) return fused_launch<D, 8, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
         return hipErrorNotSupported;
     }
 }
@@ -2020,12 +2036,26 @@ hipError_t FA2_TILE_LAUNCH(launch_bwd_fused)(int D, const float* q, const float*
                                 const float* lse, const float* delta, float* dq, float* dk, float* dv, int bh, int S,
                                 hipStream_t stream) {
     if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
+    float* dl = const_cast<float*>(delta);  // read only (no O given)
     switch (D) {
-        case 32: return fused_dispatch<32>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
-        case 64: return fused_dispatch<64>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        case 32: return fused_dispatch<32>(q, k, v, dout, lse, dl, dq, dk, dv, bh, S, nullptr, stream);
+        case 64: return fused_dispatch<64>(q, k, v, dout, lse, dl, dq, dk, dv, bh, S, nullptr, stream);
         default: return hipErrorNotSupported;
     }
 }
+
+namespace {
+// the fused launch with Δ computed inside it from O (written to delta)
+hipError_t launch_bwd_fused_delta(int D, const float* q, const float* k, const float* v, const float* o,
+                                  const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
+                                  int bh, int S, hipStream_t stream) {
+    switch (D) {
+        case 32: return fused_dispatch<32>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
+        case 64: return fused_dispatch<64>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
+        default: return hipErrorNotSupported;
+    }
+}
+}  // namespace
 
 namespace {
 template <int D>
@@ -2084,6 +2114,15 @@ hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* 
     int fused = tune_knob("BWD_FUSED", -1);
     if (fused < 0) fused = bh > 0 && S > 0 && auto_waves((long)bh * ((S + 31) / 32), 8) < 8;
     if (D <= 64 && bh > 0 && S > 0 && fused == 1) {
+        // Δ inside the fused launch below 4 blocks of 32 rows per CU (override
+        // BWD_FUSED_DELTA; 0 = the separate Δ kernel first).  Measured (B2_H8_D64 fwd +
+        // bwd, r02): S = 512 29.9 -> 26.7 us, S = 1024 45.0 -> 40.8; at S = 2048 (4
+        // blocks per CU) the dK/dV role's O reads cost more than the Δ kernel (+4 %).
+        const int dfl = auto_waves((long)bh * ((S + 31) / 32), 8) <= 2;
+        if (tune_knob("BWD_FUSED_DELTA", dfl)) {
+            const hipError_t e = launch_bwd_fused_delta(D, q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, stream);
+            if (e != hipErrorNotSupported) return e;
+        }
         hipError_t e = launch_delta(D, dout, o, delta, bh, S, stream);
         if (e != hipSuccess) return e;
         e = FA2_TILE_LAUNCH(launch_bwd_fused)(D, q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);

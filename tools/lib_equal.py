@@ -38,7 +38,9 @@ def main():
         ref = outs[default]
         for path in args.libs:
             same = [torch.equal(a, b) for a, b in zip(ref, outs[path])]
-            print(sh, os.path.basename(os.path.dirname(path)) or path, "o lse dq dk dv equal:", same)
+            diff = [float((a - b).abs().max()) for a, b in zip(ref, outs[path])]
+            print(sh, os.path.basename(os.path.dirname(path)) or path, "o lse dq dk dv equal:", same,
+                  "max abs diff:", ["%.2e" % d for d in diff])
             bad += not all(same)
     fa2amd.use_library(default)
     sys.exit(1 if bad else 0)
