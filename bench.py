@@ -65,7 +65,7 @@ def log(*a):
 
 
 # kernel-name prefixes in the rocprofv3 PMC summary
-PMC_PREFIX = {"fwd": "fa2_fwd_f16", "bwd": "fa2_bwd_onepass_f16", "bwd32": "fa2_bwd_f32"}
+PMC_PREFIX = {"fwd": "fa2_fwd_f16", "dq": "fa2_bwd_dq_f16", "dkdv": "fa2_bwd_dkdv_f16", "bwd32": "fa2_bwd_f32"}
 
 
 def traffic_from_profile(kernel: str, D: int, S: int, heads: int):
@@ -384,7 +384,13 @@ def main():
     dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
     stream = torch.cuda.current_stream(dev)
     prec = args.precision
-    kernels = ["fwd", "bwd"]
+    # fa2_backward's plan on full grids at fp16 (>= 8 blocks of 32 rows per CU, D <= 64
+    # as at C3 / C5): the dQ kernel (Δ fused) then the dK/dV kernel.  The roofline region
+    # times those two launches separately through their split entry points (the same
+    # kernel instances fa2_backward launches); otherwise the backward as one unit.
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    split_bwd = prec == "fp16" and D <= 64 and heads * ((S + 31) // 32) >= 8 * ncu
+    kernels = ["fwd", "dq", "dkdv"] if split_bwd else ["fwd", "bwd"]
 
     def step(ev=None):
         def mark(i):
@@ -393,6 +399,12 @@ def main():
         mark(0)
         fa2amd.forward(q, k, v, prec, out=o, lse=lse, stream=stream)
         mark(1)
+        if ev is not None and split_bwd:
+            fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq, stream=stream)
+            mark(2)
+            fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv, stream=stream)
+            mark(3)
+            return
         fa2amd.backward(q, k, v, o, do, lse, prec, dq=dq, dk=dk, dv=dv, delta_buf=dl, stream=stream)
         mark(2)
 
@@ -441,9 +453,10 @@ def main():
     hbm_bytes = (48.0 * S * D + 8.0 * S) * total_heads * args.steps  # fwd 16SD+4S, bwd 32SD+4S per head
     ms_per_step = elapsed / args.steps * 1e3
 
-    # dominant launch and its algorithmic FLOPs (fwd 4 S^2 D, bwd 10 S^2 D per head);
-    # at C3 fa2_backward is one launch (the one-pass kernel)
-    alg = {"fwd": 4.0, "bwd": 10.0}
+    # dominant launch and its algorithmic FLOPs per head: fwd 4 S^2 D; dK/dV 8 S^2 D (S,
+    # dP, dV, dK: four of the backward's five GEMMs); dQ 2 S^2 D (its S and dP recompute
+    # earns nothing); a whole backward 10 S^2 D
+    alg = {"fwd": 4.0, "dq": 2.0, "dkdv": 8.0, "bwd": 10.0}
     dom = max(kms, key=kms.get)
     dom_flops = alg[dom] * per_head * heads
     peak = MFMA_F16_PEAK_TFLOPS if prec in ("fp16", "bf16") else MFMA_F32_PEAK_TFLOPS
@@ -452,6 +465,7 @@ def main():
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "kernel_ms": {n: round(x, 4) for n, x in kms.items()},
+            "bwd_tflops": round(10.0 * per_head * heads / (sum(kms[n] for n in kms if n != "fwd") * 1e-3) / 1e12, 2),
             "ms_per_step_with_events": round(elapsed_ev / args.steps * 1e3, 4)}
 
     cpu = None

@@ -99,6 +99,8 @@ def _load(path):
         "fa2_device_count": [],
     }
     for name, args in sig.items():
+        if path != LIB_PATH and not hasattr(L, name):
+            continue  # an older build A/B'd by tools/kbench.py may lack newer entry points
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = ctypes.c_char_p if name == "fa2_last_error" else I
@@ -117,7 +119,10 @@ def version() -> int:
 def tune_set(knob, value: int = 0):
     """Launch-plan override (tests and tools only; fa2_tune_set): ``tune_set(None)``
     clears every override.  Nothing is read from the environment."""
-    _check(lib().fa2_tune_set(None if knob is None else knob.encode(), int(value)))
+    L = lib()
+    if knob is None and not hasattr(L, "fa2_tune_set"):
+        return  # an older build (tools/kbench.py A/B) has no overrides to clear
+    _check(L.fa2_tune_set(None if knob is None else knob.encode(), int(value)))
 
 
 class tuned:

@@ -2103,11 +2103,14 @@ hipError_t FA2_TILE_LAUNCH(launch_bwd_onepass)(int D, const float* q, const floa
 hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream) {
-    // The one-pass launch wherever it applies and its grid of 256-key items fills the
-    // chip (override BWD_ONEPASS: 1 = wherever it applies, 0 = never).
-    const int onepass = tune_knob("BWD_ONEPASS", -1);
-    if (D <= 64 && bh > 0 && S > 0 && onepass != 0 &&
-        (onepass == 1 || (long)bh * ((S + fa2f16b::OP_KEYS - 1) / fa2f16b::OP_KEYS) >= cu_count())) {
+    // The one-pass launch only on request (override BWD_ONEPASS = 1, wherever it
+    // applies).  A/B in one process on one board (r02, fa2_backward, 7 rounds):
+    // C3 dO = ones 246.7 vs 234.1 us for the two kernels, dO ~ N(0,1) 257.4 vs 255.2;
+    // B16_H16_S2048 965 vs 952; B2_H8_S4096 222.5 vs 217.9 (ones), 238.0 vs 238.2
+    // (randn).  The two kernels recompute S and dP but need no cross-workgroup hand-off
+    // and re-read Q / dO / O from L2 far less (PMC: 0.4 vs 1.46 GB per C3 backward).
+    const int onepass = tune_knob("BWD_ONEPASS", 0);
+    if (D <= 64 && bh > 0 && S > 0 && onepass == 1) {
         const hipError_t e = FA2_TILE_LAUNCH(launch_bwd_onepass)(D, q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, stream);
         if (e != hipErrorNotSupported) return e;
     }
