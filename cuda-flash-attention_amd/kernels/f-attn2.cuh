@@ -120,8 +120,9 @@ hipError_t launch_bwd_dq_delta_bf16(int D, const float* q, const float* k, const
                                     hipStream_t stream);
 
 // dK, dV and dQ in ONE persistent launch (fp16 / bf16 tiles, D <= 64; what
-// launch_backward_* runs on grids that fill the chip), or hipErrorNotSupported where it
-// does not apply.  Uses bwd_workspace(stream).
+// launch_backward_* runs when the BWD_ONEPASS override is 1 -- by default it runs the
+// two kernels, measured faster), or hipErrorNotSupported where it does
+// not apply.  Uses bwd_workspace(stream).
 hipError_t launch_bwd_onepass_f16(int D, const float* q, const float* k, const float* v, const float* o,
                                   const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                   int bh, int S, hipStream_t stream);

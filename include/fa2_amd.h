@@ -53,8 +53,11 @@ int fa2_delta(const float* dout, const float* o, float* delta, int batch, int he
               void* stream);
 
 /* Backward: dQ, dK, dV (fully overwritten; no pre-zeroing needed).  `delta` is
- * [B,H,S] scratch that receives Δ.  Replaces the device half of
- * host_flash_attention2_backward[_fp16] (kernels/f-attn2.cuh:26-41 / :56-71) and
+ * [B,H,S] scratch that receives Δ.  Determinism: FA2_FP16 / FA2_BF16 results are
+ * bitwise reproducible (no float atomics in any launch plan).  FA2_FP32 adds dQ with
+ * fp32 global atomics, as the reference does (f-attn2-backward.cu:298), so its dQ
+ * may differ in the last bits between calls; its dK and dV are reproducible.
+ * Replaces the device half of host_flash_attention2_backward[_fp16] (kernels/f-attn2.cuh:26-41 / :56-71) and
  * the CuPy launches of D_computation_reduction_kernel_wrapper +
  * flash_attention2_backward_kernel_wrapper (f-attn2-backward.cu:491-528). */
 int fa2_backward(const float* q, const float* k, const float* v, const float* o, const float* dout,
@@ -62,7 +65,7 @@ int fa2_backward(const float* q, const float* k, const float* v, const float* o,
                  int head_dim, int precision, void* stream);
 
 /* The two MFMA kernels of the fp16 backward, separately (profiling/bench hooks;
- * fa2_backward with FA2_FP16 = fa2_delta + these two). */
+ * fa2_delta + these two compute what fa2_backward with FA2_FP16 does). */
 int fa2_backward_dkdv(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                       const float* delta, float* dk, float* dv, int batch, int heads, int seq, int head_dim,
                       void* stream);
@@ -71,8 +74,10 @@ int fa2_backward_dq(const float* q, const float* k, const float* v, const float*
 /* dQ with Δ computed in the same kernel (from O and dO) and written to `delta`
  * (B*H*S floats); fa2_backward_dkdv launched after it reads that Δ.  This pair is
  * what fa2_backward runs for FA2_FP16 / FA2_BF16 on grids of at least 8 blocks of 32
- * rows per CU; on smaller grids (D <= 64) it runs fa2_delta and then ONE launch whose
- * workgroups take the dK/dV or the dQ role side by side (FA2_TUNE_BWD_FUSED). */
+ * rows per CU and at D = 128; on smaller grids (D <= 64) it runs ONE launch whose
+ * workgroups take the dK/dV or the dQ role side by side (BWD_FUSED; Δ computed inside
+ * it below 4 blocks per CU, else fa2_delta first).  BWD_ONEPASS = 1 selects the
+ * one-pass persistent kernel instead (D <= 64). */
 int fa2_backward_dq_delta(const float* q, const float* k, const float* v, const float* o, const float* dout,
                           const float* lse, float* delta, float* dq, int batch, int heads, int seq, int head_dim,
                           void* stream);
