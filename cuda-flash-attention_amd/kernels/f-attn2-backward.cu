@@ -75,9 +75,12 @@ __device__ __forceinline__ void delta_row_body(const float* __restrict__ dO, con
 }
 
 // Library Δ kernel: D/4 lanes per row (float4 loads), grid-stride over rows.
+// zero != nullptr: also clears those rows of `zero` (the fp32 backward's dQ, which its
+// kernel then accumulates with atomics): one launch instead of a memset and Δ.
 template <int D>
 __global__ void __launch_bounds__(256) fa2_delta_kernel(const float* __restrict__ dO, const float* __restrict__ O,
-                                                        float* __restrict__ Dvec, long rows) {
+                                                        float* __restrict__ Dvec, long rows,
+                                                        float* __restrict__ zero = nullptr) {
     constexpr int LPR = D / 4;  // lanes per row
     const long stride = (long)gridDim.x * (256 / LPR);
     const int sub = threadIdx.x % LPR;
@@ -88,6 +91,7 @@ __global__ void __launch_bounds__(256) fa2_delta_kernel(const float* __restrict_
 #pragma unroll
         for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
         if (sub == 0) Dvec[row] = acc;
+        if (zero) *reinterpret_cast<f32x4*>(zero + row * D + 4 * sub) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 }
 
@@ -270,13 +274,14 @@ namespace fa2 {
 
 namespace {
 template <int D>
-hipError_t delta_dispatch(const float* dout, const float* o, float* delta, int bh, int S, hipStream_t stream) {
+hipError_t delta_dispatch(const float* dout, const float* o, float* delta, int bh, int S, hipStream_t stream,
+                          float* zero = nullptr) {
     const long rows = (long)bh * S;
     const long rows_per_block = 256 / (D / 4);
     long grid = (rows + rows_per_block - 1) / rows_per_block;
     if (grid > 8192) grid = 8192;
     hipLaunchKernelGGL((fa2f32b::fa2_delta_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, dout, o, delta,
-                       rows);
+                       rows, zero);
     return hipGetLastError();
 }
 template <int D>
@@ -304,9 +309,13 @@ hipError_t launch_backward_f32(int D, const float* q, const float* k, const floa
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream) {
     if (bh <= 0 || S <= 0 || !supported_head_dim(D)) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(dq, 0, (size_t)bh * S * D * sizeof(float), stream);
-    if (e != hipSuccess) return e;
-    e = launch_delta(D, dout, o, delta, bh, S, stream);
+    // Δ, with dQ cleared in the same pass (the kernel below adds into it)
+    hipError_t e;
+    switch (D) {
+        case 32: e = delta_dispatch<32>(dout, o, delta, bh, S, stream, dq); break;
+        case 64: e = delta_dispatch<64>(dout, o, delta, bh, S, stream, dq); break;
+        default: e = delta_dispatch<128>(dout, o, delta, bh, S, stream, dq); break;
+    }
     if (e != hipSuccess) return e;
     switch (D) {
         case 32: return bwd_f32_dispatch<32>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
