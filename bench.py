@@ -283,7 +283,33 @@ def extras(fa2amd, torch, dev):
                                             "frac_mfma_f32": round(tf / MFMA_F32_PEAK_TFLOPS, 4)}
     ms, tf, gbps = time_config(fa2amd, torch, dev, 64, 16, 2048, 64, "fp16", False, iters=10)
     out["c5_1gpu_B64_H16_S2048_D64_fp16_fwdbwd"] = roof_entry(ms, tf, gbps, 2048, False)
+    out["c3_host_api_pcie_inclusive"] = host_api_entry(fa2amd, 4, 16, 2048, 64)
     return out
+
+
+def host_api_entry(fa2amd, B, H, S, D, runs=3):
+    """The reference's host-buffer boundary (host_flash_attention2_{forward,backward}_fp16
+    semantics through fa2_{forward,backward}_host): per call device alloc, H2D, kernels,
+    D2H, free.  Wall time of fwd + bwd from host arrays (PCIe-inclusive; reported beside
+    the HBM-resident `value`, never as it) and the kernel-only ms the calls report."""
+    gen = np.random.default_rng(3)
+    q, k, v = (gen.random((B, H, S, D), dtype=np.float32) for _ in range(3))
+    do = np.ones_like(q)
+    walls, kms = [], []
+    for i in range(runs + 1):
+        t0 = time.perf_counter()
+        o, lse, kf = fa2amd.forward_host(q, k, v, "fp16")
+        _, _, _, kb = fa2amd.backward_host(q, k, v, o, do, lse, "fp16")
+        if i:  # the first call pays the device-allocator warm-up
+            walls.append(time.perf_counter() - t0)
+            kms.append(kf + kb)
+    wall, km = statistics.median(walls), statistics.median(kms)
+    flops = 14.0 * B * H * S * S * D
+    return {"wall_ms": round(wall * 1e3, 3), "tflops_wall": round(flops / wall / 1e12, 2), "kernel_ms": round(km, 4),
+            "tflops_kernels": round(flops / (km * 1e-3) / 1e12, 2),
+            "h2d_d2h_bytes": 4 * B * H * S * D * (3 + 1 + 5 + 3) + 4 * B * H * S * 2,
+            "what": "fa2_forward_host + fa2_backward_host from host numpy buffers (alloc, H2D, kernels, D2H, free "
+                    "per call), median of 3"}
 
 
 # ---------------------------------------------------------------------------
