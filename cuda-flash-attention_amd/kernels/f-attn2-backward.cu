@@ -47,6 +47,29 @@ __device__ __forceinline__ void stage_rows(float* tile, const float* __restrict_
     }
 }
 
+// stage_rows split in two (guide T14): the loads into registers, issued a compute
+// phase ahead of the LDS stores, so the L2/HBM round trip hides under MFMAs.
+template <int D, int ROWS>
+struct RowStage {
+    static constexpr int N = ROWS * (D / 4) / 256;  // f32x4 chunks per thread
+    f32x4 v[N];
+    __device__ __forceinline__ void load(const float* __restrict__ src, int row0, int S, int tid) {
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            const int x = tid + 256 * c, row = x / (D / 4), c4 = x - row * (D / 4);
+            v[c] = row0 + row < S ? *reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * D + 4 * c4)
+                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    __device__ __forceinline__ void store(float* tile, float scale, int tid) const {
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            const int x = tid + 256 * c, row = x / (D / 4), c4 = x - row * (D / 4);
+            *reinterpret_cast<f32x4*>(tile + row * (D + 4) + 4 * c4) = v[c] * scale;
+        }
+    }
+};
+
 // ---------------------------------------------------------------------------
 // Δ = rowsum(dO ∘ O).  Reference-geometry body: one row per workgroup, any
 // blockDim <= 1024 (the harness uses 64, test_flash_attention2.py:504-506).
@@ -150,21 +173,36 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
             dva[b][i] = 0.f;
         }
 
+    // Q and dO super-tiles go HBM -> registers one compute phase before they are
+    // needed (RowStage), so each LDS restage costs a barrier pair but no round trip:
+    // dO(st) loads during S(st), Q(st + 1) loads during dK / dQ(st).  Q(st) is loaded
+    // once and stored twice from the same registers: scaled for S, unscaled for dK.
     const int nsuper = (S + QS - 1) / QS;
+    RowStage<D, QS> rq, rd;
+    float rl = 0.f, rdel = 0.f;  // this thread's LSE / Δ row of the next super-tile (tid < QS)
+    auto load_rows = [&](int q0) {
+        if (tid < QS) {
+            const int qi = q0 + tid;
+            rl = qi < S ? LSE[rbase + qi] * FA2FB_LOG2E : __builtin_inff();
+            rdel = qi < S ? Delta[rbase + qi] : 0.f;
+        }
+    };
+    rq.load(Q + base, 0, S, tid);
+    load_rows(0);
+    rq.store(T, qscale, tid);
+    if (tid < QS) {
+        lse2[tid] = rl;
+        del[tid] = rdel;
+    }
+    __syncthreads();
     for (int st = 0; st < nsuper; ++st) {
         const int q0 = st * QS;
         const int qw = q0 + 32 * wave;  // this wave's 32 query rows
         const bool active = qw < S;
+        const bool more = st + 1 < nsuper;
         const float* Tw = T + 32 * wave * LD;
-        // ---- Q (scaled) + row constants
-        __syncthreads();
-        stage_rows<D>(T, Q + base, q0, QS, S, tid, qscale);
-        if (tid < QS) {
-            const int qi = q0 + tid;
-            lse2[tid] = qi < S ? LSE[rbase + qi] * FA2FB_LOG2E : __builtin_inff();
-            del[tid] = qi < S ? Delta[rbase + qi] : 0.f;
-        }
-        __syncthreads();
+        rd.load(dO + base, q0, S, tid);
+        // ---- S = Q K^T (T holds Q scaled), P
         f32x16 p;  // P[q][key]: rows q (registers), col key (lane)
         if (active) {
 #pragma unroll
@@ -181,7 +219,7 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
         }
         // ---- dO
         __syncthreads();
-        stage_rows<D>(T, dO + base, q0, QS, S, tid, 1.f);
+        rd.store(T, 1.f, tid);
         __syncthreads();
         f32x16 ds;
         if (active) {
@@ -205,10 +243,17 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
 #pragma unroll
             for (int i = 0; i < 16; ++i) Dsw[acc_row(i, h) * 33 + r] = ds[i];
         }
-        // ---- Q (unscaled) for dK
+        // ---- Q (unscaled, from the same registers) for dK; the next super-tile's row
+        // constants (lse2 / del are read only by the S and dP phases, both done)
+        if (more) load_rows(q0 + QS);
         __syncthreads();
-        stage_rows<D>(T, Q + base, q0, QS, S, tid, 1.f);
+        rq.store(T, 1.f, tid);
+        if (more && tid < QS) {
+            lse2[tid] = rl;
+            del[tid] = rdel;
+        }
         __syncthreads();
+        if (more) rq.load(Q + base, q0 + QS, S, tid);
         if (active) {
 #pragma unroll
             for (int b = 0; b < D / 32; ++b)
@@ -229,6 +274,12 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
                     if (qi < S) atomicAdd(dQ + base + (long)qi * D + 32 * b + r, acc[i] * dscale);
                 }
             }
+        }
+        // ---- the next super-tile's Q, scaled
+        if (more) {
+            __syncthreads();
+            rq.store(T, qscale, tid);
+            __syncthreads();
         }
     }
 

@@ -39,18 +39,30 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 // row index (0..31) held by accumulator register i of lane-half h (32x32 MFMA C/D map)
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-// Cooperative staging of rows [row0, row0+ROWS) of a [S][D] fp32 tensor into an
-// LDS tile with row stride D+4 (zero rows past S); 256 threads, float4 granules.
-template <int D>
-__device__ __forceinline__ void stage_rows(float* tile, const float* __restrict__ src, int row0, int ROWS, int S,
-                                           int tid) {
-    for (int x = tid; x < ROWS * (D / 4); x += 256) {
-        const int row = x / (D / 4), c4 = x - row * (D / 4);
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (row0 + row < S) v = *reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * D + 4 * c4);
-        *reinterpret_cast<f32x4*>(tile + row * (D + 4) + 4 * c4) = v;
+// Cooperative staging of rows [row0, row0+ROWS) of a [S][D] fp32 tensor into an LDS
+// tile with row stride D+4 (zero rows past S), split in two (guide T14): the loads
+// into registers one compute phase ahead of the LDS stores, so the round trip hides
+// under the MFMAs.  256 threads, float4 granules.
+template <int D, int ROWS>
+struct RowStage {
+    static constexpr int N = ROWS * (D / 4) / 256;  // f32x4 chunks per thread
+    f32x4 v[N];
+    __device__ __forceinline__ void load(const float* __restrict__ src, int row0, int S, int tid) {
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            const int x = tid + 256 * c, row = x / (D / 4), c4 = x - row * (D / 4);
+            v[c] = row0 + row < S ? *reinterpret_cast<const f32x4*>(src + (long)(row0 + row) * D + 4 * c4)
+                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
     }
-}
+    __device__ __forceinline__ void store(float* tile, int tid) const {
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            const int x = tid + 256 * c, row = x / (D / 4), c4 = x - row * (D / 4);
+            *reinterpret_cast<f32x4*>(tile + row * (D + 4) + 4 * c4) = v[c];
+        }
+    }
+};
 
 // LDS floats needed by the forward body: one [128][D+4] super-tile (K, then V)
 // or, for the final merge, 4 waves x 32 rows x (D+4) plus (m, l) pairs.
@@ -97,15 +109,21 @@ __device__ __forceinline__ void fwd_f32_body(const float* __restrict__ Q, const 
         for (int i = 0; i < 16; ++i) oacc[b][i] = 0.f;
     float m_run = -__builtin_inff(), l_run = 0.f;
 
+    // K and V super-tiles go HBM -> registers one phase ahead of their LDS stores
+    // (RowStage): V(st) loads during the score phase of st, K(st + 1) during its PV
+    // phase, so each restage costs a barrier pair but no exposed round trip.
     const int nsuper = (S + KS - 1) / KS;
+    RowStage<D, KS> rk, rv;
+    rk.load(K + base, 0, S, tid);
     for (int st = 0; st < nsuper; ++st) {
         const int k0 = st * KS;
         const int kw = k0 + 32 * wave;  // this wave's 32-key sub-tile
         const float* Tw = smem + 32 * wave * LD;
         // ---- K phase
         __syncthreads();
-        stage_rows<D>(smem, K + base, k0, KS, S, tid);
+        rk.store(smem, tid);
         __syncthreads();
+        rv.load(V + base, k0, S, tid);
         f32x16 sacc;
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
@@ -143,8 +161,9 @@ __device__ __forceinline__ void fwd_f32_body(const float* __restrict__ Q, const 
         }
         // ---- V phase
         __syncthreads();
-        stage_rows<D>(smem, V + base, k0, KS, S, tid);
+        rv.store(smem, tid);
         __syncthreads();
+        if (st + 1 < nsuper) rk.load(K + base, k0 + KS, S, tid);
         if (kw < S) {
             // O^T += V^T P^T : step i uses accumulator register i as B (k = h <-> key acc_row(i,h))
 #pragma unroll
