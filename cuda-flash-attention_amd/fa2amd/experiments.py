@@ -338,6 +338,45 @@ def plot(rows, out_dir):
     path = os.path.join(out_dir, "kernel_comparison.png")
     fig.savefig(path, dpi=120)
     plt.close(fig)
+    if any("seqlen" in r.test.lower() for r in ok):
+        plot_seqlen(ok, out_dir, plt)
+    return path
+
+
+def plot_seqlen(ok, out_dir, plt):
+    """seqlen_analysis.png for the SeqLen-* rows: TFLOPS, bandwidth, speedup over
+    PyTorch and time against S, one line per kernel (the harness's
+    _generate_seqlen_plots, test_flash_attention2.py:1207-1287)."""
+    rows = sorted((r for r in ok if "seqlen" in r.test.lower()), key=lambda r: r.S)
+    kernels = sorted({r.kernel for r in rows})
+    seqs = sorted({r.S for r in rows})
+    panels = (("TFLOPS", lambda r: r.metrics.get("tflops", 0.0), "o", False),
+              ("Bandwidth (GB/s)", lambda r: r.metrics.get("bandwidth_gbps", 0.0), "s", False),
+              ("Speedup vs PyTorch", lambda r: r.metrics.get("speedup", 0.0), "^", False),
+              ("Execution Time (ms)", lambda r: r.kernel_ms, "d", True))
+    fig, axes = plt.subplots(2, 2, figsize=(16, 12))
+    for ax, (label, get, marker, logy) in zip(axes.flat, panels):
+        for kern in kernels:
+            kr = [r for r in rows if r.kernel == kern]
+            ax.plot([r.S for r in kr], [get(r) for r in kr], marker=marker, linewidth=2, markersize=6,
+                    label=kern.upper())
+        if label.startswith("Speedup"):
+            ax.axhline(y=1.0, color="r", linestyle="--", linewidth=1, alpha=0.5)
+        ax.set_xlabel("Sequence Length")
+        ax.set_ylabel(label)
+        ax.set_title(f"{label.split(' (')[0]} vs Sequence Length")
+        ax.set_xscale("log", base=2)
+        ax.set_xticks(seqs)
+        ax.set_xticklabels([str(x) for x in seqs])
+        if logy:
+            ax.set_yscale("log")
+        ax.legend(fontsize=9)
+        ax.grid(True, alpha=0.3, which="both")
+    fig.suptitle("Sequence Length Scaling Analysis (MI355X)")
+    fig.tight_layout()
+    path = os.path.join(out_dir, "seqlen_analysis.png")
+    fig.savefig(path, dpi=120)
+    plt.close(fig)
     return path
 
 

@@ -224,3 +224,23 @@ def test_experiment_cli_flags(monkeypatch, tmp_path):
     calls.clear()
     assert experiments.main(["--mode", "backward", "--configs", "Small-1"]) == 0
     assert calls == [("backward", "Small-1", True)]
+
+
+def test_experiment_seqlen_plot(monkeypatch, tmp_path):
+    """--seqlen-experiment --save-results writes seqlen_analysis.png beside the CSV and
+    kernel_comparison.png, as the harness's _generate_seqlen_plots does
+    (test_flash_attention2.py:1204-1287); runners stubbed (no GPU here)."""
+    pytest.importorskip("matplotlib")
+    from fa2amd import experiments
+
+    def run(name, B, H, S, D, kernels, *a):
+        return [experiments.Row(name, k, "forward", B, H, S, D, True,
+                                {"max_abs_error": 0.0, "tflops": 1e-3 * S, "bandwidth_gbps": 1.0, "speedup": 2.0},
+                                1e-4 * S, 1.0) for k in kernels]
+
+    monkeypatch.setattr(experiments, "run_forward", run)
+    assert experiments.main(["--seqlen-experiment", "--save-results", "--output-dir", str(tmp_path)]) == 0
+    for f in ("experiment_results.csv", "kernel_comparison.png", "seqlen_analysis.png"):
+        assert (tmp_path / f).stat().st_size > 0, f
+    lines = (tmp_path / "experiment_results.csv").read_text().splitlines()
+    assert sorted({int(ln.split(",")[5]) for ln in lines[1:]}) == list(experiments.SEQLEN_SWEEP)
