@@ -741,11 +741,17 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     // 4 ways instead of shrinking the workgroup -- 8 waves on 64 query rows, or 4 waves
     // on 32 rows below 2 query blocks per CU.  Measured (B2_H8_D64 fwd, r01):
     // S = 512 12.4 -> 9.9 us, S = 1024 21.4 -> 15.4 us; at S = 2048 (4 blocks per CU)
-    // KS = 2 on 32-key tiles ties the unsplit 4-wave kernel (35.9 vs 34.8 us).
+    // KS = 2 on 32-key tiles tied the unsplit 4-wave kernel in r01 (35.9 vs 34.8 us).
+    // With 4-8 blocks per CU, D = 64 splits the key range 2 ways at 8 waves (r02, fwd +
+    // bwd step, 15 rounds: B2_H8_S2048 100.6 -> 99.3 us with dO = ones, 104.3 -> 103.1
+    // with dO ~ N(0,1)); D = 32 stays unsplit at 4 waves (the split measured +5.5 %).
     int ks = tune_knob("FWD_KS", 0);
     if (ks == 0 && nw == 0 && D <= 64 && auto_waves(units, 8) == 2) {
         ks = 4;
         nw = auto_waves(units, 2, 1) == 2 ? 8 : 4;
+    } else if (ks == 0 && nw == 0 && D == 64 && auto_waves(units, 8) == 4) {
+        ks = 2;
+        nw = 8;
     }
     if (nw == 0) nw = auto_waves(units, 8);
     if constexpr (D <= 64) {
