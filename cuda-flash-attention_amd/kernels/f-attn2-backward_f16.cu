@@ -1999,8 +1999,7 @@ hipError_t fused_launch(const float* q, const float* k, const float* v, const fl
     return hipGetLastError();
 }
 // The fused dK/dV + dQ launch for D <= 64, or hipErrorNotSupported (then the caller
-// runs the two kernels).  Split factors follow the separate kernels' auto rule:
-// below 4 blocks of 32 rows per CU QS = 2 / KS = 4 (32-key tiles), below 8 QS = 2 /
+// runs the two kernels).  Split factors: below 8 blocks of 32 rows per CU QS = 2 /
 // KS = 2, else unsplit.  Overrides (fa2_tune_set): BWD_FQS, BWD_FKS, BWD_FNW.
 template <int D>
 hipError_t fused_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
@@ -2014,8 +2013,11 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
         // below 2 blocks per CU: 4-wave roles, KS = 2 (B2_H8_S512: bwd 16.7 -> 15.7 us;
         // at 2 blocks per CU, B2_H8_S1024, that geometry is 21 % slower than 8 waves)
         const bool tiny = a == 2 && auto_waves(units, 2, 1) == 1;
+        // dQ role KS = 2 on every split grid (r02: below 4 blocks per CU KS = 2 beat the
+        // r01 choice KS = 4 by 4.6-7.5 % on the fwd + bwd step, B2_H8_S1024 D = 32 / 64,
+        // B4_H8_S512, B1_H16_S1024, S = 1000, both dO distributions)
         const int fqs = tune_knob("BWD_FQS", a == 8 ? 1 : 2);
-        const int fks = tune_knob("BWD_FKS", a == 8 ? 1 : (a == 4 || tiny) ? 2 : 4);
+        const int fks = tune_knob("BWD_FKS", a == 8 ? 1 : 2);
         // waves per workgroup of both roles (8, or 4 for the split pairs)
         const int fnw = tune_knob("BWD_FNW", tiny ? 4 : 8);
         if (fqs == 1 && fks == 1) return fused_launch<D, 8, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
