@@ -40,8 +40,8 @@ def main():
                                                     (lse, "lse", 3)), B, H, S, D, dev),
         "checks (10 tensors)": lambda: fa2amd._ptrs(bnamed, B, H, S, D, dev),
         "stream lookup": lambda: fa2amd._stream(None, dev),
-        "ctypes fa2_forward": lambda: L.fa2_forward(*fptrs, B, H, S, D, 1, st),
-        "ctypes fa2_backward": lambda: L.fa2_backward(*bptrs, B, H, S, D, 1, st),
+        "ctypes fa2_forward": lambda: L.fa2_forward(*fptrs, B, H, S, D, fa2amd.FA2_FP16, st),
+        "ctypes fa2_backward": lambda: L.fa2_backward(*bptrs, B, H, S, D, fa2amd.FA2_FP16, st),
     }
     for name, f in cases.items():
         f()
