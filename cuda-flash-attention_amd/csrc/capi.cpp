@@ -68,6 +68,17 @@ namespace {
 std::mutex g_tune_mu;
 std::vector<std::pair<std::string, int>> g_tune;
 std::atomic<int> g_tune_n{0};
+
+// the launch-plan overrides the launchers read (fa2_tune_set rejects other names,
+// so a misspelt knob cannot silently leave an A/B on the default plan)
+const char* const kKnobs[] = {"FWD_WAVES", "FWD_KS",    "DKDV_WAVES", "DKDV_QS", "DQ_WAVES",        "DQ_KS",
+                              "BWD_FUSED", "BWD_FUSED_DELTA", "BWD_FQS", "BWD_FKS", "BWD_FNW",
+                              "HOST_SHARDS_ON_DEVICE0"};
+bool known_knob(const char* k) {
+    for (const char* n : kKnobs)
+        if (!strcmp(n, k)) return true;
+    return false;
+}
 }  // namespace
 
 namespace fa2 {
@@ -93,59 +104,6 @@ int cu_count() {
     return ncu;
 }
 
-namespace {
-struct Workspace {
-    int device;
-    hipStream_t stream;
-    void* ptr;
-    size_t bytes;
-};
-std::mutex g_ws_mu;
-std::vector<Workspace> g_ws;
-}  // namespace
-
-void* bwd_workspace(hipStream_t stream, size_t bytes) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lock(g_ws_mu);
-    Workspace* w = nullptr;
-    for (auto& e : g_ws)
-        if (e.device == dev && e.stream == stream) w = &e;
-    if (w && w->bytes >= bytes) return w->ptr;
-    // (re)allocation: never inside a graph capture (the caller then takes another plan)
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    const size_t want = std::max(bytes, w ? 2 * w->bytes : (size_t)1 << 16);
-    void* p = nullptr;
-    if (hipMalloc(&p, want) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, want) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-        (void)hipFree(p);
-        return nullptr;
-    }
-    if (w) {
-        (void)hipStreamSynchronize(stream);  // the old block may still be in use there
-        (void)hipFree(w->ptr);
-        w->ptr = p;
-        w->bytes = want;
-    } else {
-        g_ws.push_back({dev, stream, p, want});
-    }
-    return p;
-}
-
-void release_workspace(hipStream_t stream) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return;
-    std::lock_guard<std::mutex> lock(g_ws_mu);
-    for (size_t i = 0; i < g_ws.size(); ++i)
-        if (g_ws[i].device == dev && g_ws[i].stream == stream) {
-            (void)hipStreamSynchronize(stream);
-            (void)hipFree(g_ws[i].ptr);
-            g_ws.erase(g_ws.begin() + i);
-            return;
-        }
-}
-
 int auto_waves(long blocks32, int maxnw, int minnw) {
     const int ncu = cu_count();
     for (int nw = maxnw; nw > minnw; nw /= 2)
@@ -156,14 +114,14 @@ int auto_waves(long blocks32, int maxnw, int minnw) {
 
 extern "C" {
 
-int fa2_version(void) { return 1 * 10000 + 1 * 100 + 0; }
+int fa2_version(void) { return 1 * 10000 + 2 * 100 + 0; }
 
 int fa2_tune_set(const char* knob, int value) {
+    if (knob && !known_knob(knob)) return fail(FA2_E_INVALID, "unknown knob name");
     std::lock_guard<std::mutex> lock(g_tune_mu);
     if (!knob) {
         g_tune.clear();
     } else {
-        if (!*knob || strlen(knob) > 32) return fail(FA2_E_INVALID, "bad knob name");
         bool found = false;
         for (auto& kv : g_tune)
             if (kv.first == knob) kv.second = value, found = true;
@@ -171,6 +129,17 @@ int fa2_tune_set(const char* knob, int value) {
     }
     g_tune_n.store((int)g_tune.size(), std::memory_order_release);
     return FA2_OK;
+}
+
+int fa2_tune_get(const char* knob, int* value) {
+    if (!knob || !known_knob(knob)) return fail(FA2_E_INVALID, "unknown knob name");
+    std::lock_guard<std::mutex> lock(g_tune_mu);
+    for (const auto& kv : g_tune)
+        if (kv.first == knob) {
+            if (value) *value = kv.second;
+            return 1;
+        }
+    return 0;
 }
 
 const char* fa2_last_error(void) { return g_err.c_str(); }
@@ -296,10 +265,7 @@ int run_shard(HostJob& j) {
     if ((rc = hip_status(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
     struct StreamGuard {
         hipStream_t s;
-        ~StreamGuard() {
-            fa2::release_workspace(s);
-            (void)hipStreamDestroy(s);
-        }
+        ~StreamGuard() { (void)hipStreamDestroy(s); }
     } sg{st};
     hipEvent_t e0, e1;
     if ((rc = hip_status(hipEventCreate(&e0), "hipEventCreate"))) return rc;

@@ -34,9 +34,12 @@ SUPPORTED_HEAD_DIMS = (32, 64, 128)
 C_SYMBOLS = (
     "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv", "fa2_backward_dq", "fa2_backward_dq_delta",
     "fa2_naive_forward", "fa2_fa1_forward",
-    "fa2_forward_host", "fa2_backward_host", "fa2_shard_range", "fa2_tune_set", "fa2_last_error",
+    "fa2_forward_host", "fa2_backward_host", "fa2_shard_range", "fa2_tune_set", "fa2_tune_get", "fa2_last_error",
     "fa2_version", "fa2_device_count",
 )
+# launch-plan overrides fa2_tune_set accepts (include/fa2_amd.h)
+KNOBS = ("FWD_WAVES", "FWD_KS", "DKDV_WAVES", "DKDV_QS", "DQ_WAVES", "DQ_KS", "BWD_FUSED", "BWD_FUSED_DELTA",
+         "BWD_FQS", "BWD_FKS", "BWD_FNW", "HOST_SHARDS_ON_DEVICE0")
 
 
 class FA2Error(RuntimeError):
@@ -94,6 +97,7 @@ def _load(path):
         "fa2_backward_host": [P] * 9 + [I] * 6 + [FP],
         "fa2_shard_range": [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)],
         "fa2_tune_set": [ctypes.c_char_p, I],
+        "fa2_tune_get": [ctypes.c_char_p, ctypes.POINTER(I)],
         "fa2_last_error": [],
         "fa2_version": [],
         "fa2_device_count": [],
@@ -125,20 +129,35 @@ def tune_set(knob, value: int = 0):
     _check(L.fa2_tune_set(None if knob is None else knob.encode(), int(value)))
 
 
+def tune_get(knob):
+    """The override set for ``knob`` (fa2_tune_get), or None when it has none."""
+    v = ctypes.c_int(0)
+    rc = lib().fa2_tune_get(knob.encode(), ctypes.byref(v))
+    if rc < 0:
+        _check(rc)
+    return v.value if rc == 1 else None
+
+
 class tuned:
-    """``with fa2amd.tuned(DKDV_QS=2, DKDV_WAVES=8): ...`` -- overrides for the block,
-    cleared on exit."""
+    """``with fa2amd.tuned(DKDV_QS=2, DKDV_WAVES=8): ...`` -- overrides for the block;
+    on exit every override is back to what it was before the block (nested blocks and
+    overrides set outside keep their values)."""
 
     def __init__(self, **knobs):
         self.knobs = knobs
+        self.saved = None
 
     def __enter__(self):
+        self.saved = {k: tune_get(k) for k in KNOBS}
         for k, v in self.knobs.items():
             tune_set(k, v)
         return self
 
     def __exit__(self, *exc):
         tune_set(None)
+        for k, v in self.saved.items():
+            if v is not None:
+                tune_set(k, v)
         return False
 
 

@@ -1196,475 +1196,6 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
                                            O);
 }
 
-// ===========================================================================
-// One-pass backward: dK, dV and dQ from ONE persistent launch (D <= 64)
-// ===========================================================================
-// The dK/dV kernel's work unit (8 waves x 32 keys of one (b, h) head, the head's
-// 64-query steps streamed through LDS) also produces everything dQ needs: each
-// step's dS -- already packed to fp16 as the dKᵀ operand -- goes to an LDS image
-// [256 keys][64 queries], and at the start of the next step the workgroup computes
-// dQᵀ_part = Kᵀ · dSᵀ for those 64 queries over its 256 keys on 16x16x32 (Kᵀ by
-// transposed reads of an LDS image of K kept for the whole item).  Nothing is
-// recomputed: 5 GEMMs of 2·S²D FLOPs, as the algorithm has them (the two-kernel
-// plan runs 6: S and dP twice), and Q, dO, K, V leave HBM once per item instead of
-// once per kernel (reference: dQ by atomics, f-attn2-backward.cu:269-301).
-//
-// Summing dQ over the head's NKB = ceil(S / 256) key blocks: a fixed chain order per
-// query step, the running sum handed over in dQ itself.  A wave stores its rows of
-// the sum write-through (sc1, 16 B per lane), drains them (s_waitcnt vmcnt(0)), then
-// one lane stores an sc1 flag; the same wave of the next key block polls that flag
-// relaxed and reads the sum with sc1 loads (cdna_hip_programming.md Guideline 16 R1;
-// MI355X_MICROARCH §visibility, table row 1, with the wave as the storing unit: a
-// wave only ever hands over the dQ rows it computed).  Fixed order: dQ is bitwise
-// reproducible, and no float atomics (gfx950 runs those memory-side at ≈1.3 TB/s;
-// at C3 they would be 256 MiB of adds, a 200 us floor).
-//   Rotation: key block k sweeps the query steps from off_k = floor(k·NQS/NKB) on,
-// wrapping around, so the chain of step q -- the blocks in the order they reach
-// it -- has about NQS/NKB steps between neighbours.  Block k's position in the chain
-// of q is (k* - k) mod NKB, k* = the last block with off_k <= q.  The hop of step t
-// runs during step t + 1 (flag polled at the step's start, the running sum loaded
-// mid-step, added and passed on at its end), so the hop latency hides under MFMAs.
-//   Persistent: grid = one workgroup per CU (the LDS block is > 80 KB); items
-// (head, key block) come from 8 per-XCD queues (heads h ≡ x mod 8 on queue x, so a
-// head's blocks share an XCD's L2 for Q, dO and O), and a workgroup whose queue is
-// empty steals from the others.  A queue hands out items in order, so at most one
-// head per queue is partly handed out and every chain predecessor of a running item
-// is running or done: no deadlock under any dispatch order or placement while the
-// grid covers every item or exceeds 8 (NKB - 1) workgroups (the launcher checks).
-// Every wait is bounded: a wait that gives up raises an abort word that ends every
-// other wait, and dQ then holds NaN -- a visible failure, never a hang.
-//   Flags carry a call epoch, advanced by the last workgroup to leave (which also
-// rewinds the queues), so no per-call memset: the workspace is zeroed once when it
-// is allocated (fa2::bwd_workspace).
-//   Δ = rowsum(dO ∘ O) is recomputed per step from O rows staged beside dO (the
-// head's other key blocks read the same rows from L2); key block 0 writes it out.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) unsigned gu32;
-
-// workspace words (u32): [0, 8) per-XCD queue heads, then these; flags from OP_WS_FLAGS
-enum { OP_WS_EXITED = 8, OP_WS_EPOCH = 9, OP_WS_ABORT = 10, OP_WS_FLAGS = 16 };
-constexpr int OP_KEYS = 256;  // keys per item: 8 waves x 32
-constexpr unsigned OP_SPIN_LIMIT = 1u << 20;
-
-__device__ __forceinline__ unsigned op_ld(unsigned* p) {
-    return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void op_st(unsigned* p, unsigned v) {
-    __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned op_add(unsigned* p, unsigned v) {
-    return __hip_atomic_fetch_add((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// bounded wait for a hop flag: one relaxed (sc1) load per pass, s_sleep between passes
-__device__ __forceinline__ bool op_wait(unsigned* flag, unsigned want, unsigned* ws, unsigned epoch) {
-    for (unsigned it = 1;; ++it) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_readfirstlane(op_ld(flag)) == want) return true;
-        if ((it & 255) == 0) {
-            if (op_ld(ws + OP_WS_ABORT) == epoch + 1) return false;
-            if (it >= OP_SPIN_LIMIT) {
-                op_st(ws + OP_WS_ABORT, epoch + 1);
-                return false;
-            }
-        }
-    }
-}
-
-template <int D>
-struct OpLds {
-    static constexpr int QT = 64, TILE = QT * D;   // halves
-    static constexpr int KI = 4 * TILE;            // [buf][Q | dO] tiles, then the K image [256][D]
-    static constexpr int DSI = KI + OP_KEYS * D;   // [2] dSᵀ images [256 keys][64 queries]
-    static constexpr int DSIMG = OP_KEYS * QT;
-    static constexpr int HALVES = DSI + 2 * DSIMG;
-    static constexpr int ROWS = 2 * HALVES;        // bytes: [2][-lse2 | -delta][64] fp32
-    static constexpr int MISC = ROWS + 2 * 2 * QT * 4;
-    static constexpr int BYTES = MISC + 16;
-    static_assert(8 * 32 * 36 * 4 <= 2 * 2 * DSIMG, "the epilogue stage fits over the dS images");
-};
-
-// Per-lane offsets of the one-pass kernel's own accesses.  Wave w owns the dQ tiles of
-// queries 16 (w & 3) .. +15 of a step and d-blocks (w >> 2) D/32 .. +D/32-1 (of 16).
-template <int D>
-struct OpOffsets {
-    int dsw[2][2];    // dS write, query block qb, k-slots 4h..4h+3: row key (l & 15), col qb*32 + 16h + 4g
-    int ka[D / 32][2];  // transposed K-image reads (rows 4g + q / 16 + 4g + q) of the wave's d-blocks
-    int db[2];        // transposed dSᵀ-image reads of the wave's 16 queries
-    int voff[D / 32];   // byte offset of the lane's 4 dQ values inside a 64-query step
-    __device__ __forceinline__ void init(int lane, int wave) {
-        const int i = lane & 15, g = lane >> 4, q = i >> 2, p4 = i & 3;
-        const int qblk = wave & 3, md0 = (wave >> 2) * (D / 32);
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) dsw[qb][h] = tile_off<64>(wave * 32 + i, qb * 32 + 16 * h + 4 * g);
-#pragma unroll
-        for (int m = 0; m < D / 32; ++m) {
-            ka[m][0] = tile_off<D>(4 * g + q, 16 * (md0 + m) + 4 * p4);
-            ka[m][1] = tile_off<D>(16 + 4 * g + q, 16 * (md0 + m) + 4 * p4);
-            voff[m] = ((16 * qblk + i) * D + 16 * (md0 + m) + 4 * g) * 4;
-        }
-        db[0] = tile_off<64>(4 * g + q, 16 * qblk + 4 * p4);
-        db[1] = tile_off<64>(16 + 4 * g + q, 16 * qblk + 4 * p4);
-    }
-};
-
-// One 64-query step for the wave's 32 keys: dkdv_step16's four products, plus the
-// step's dS (the dKᵀ B operand) written to the dSᵀ image.  kmask (the ragged key
-// block's waves only): keys >= S get an S seed of -inf, so P = dS = 0 there.
-template <int D, typename Mid>
-__device__ __forceinline__ void op_step(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
-                                        const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
-                                        const OpOffsets<D>& oo, _Float16* dsimg, int g, bool kmask, int wkey0,
-                                        int S, Mid&& mid) {
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-        if (qb == 1) mid();
-        f32x4 sa[2][2], da[2][2];  // [mb][nb]
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            const f32x4 lv = *reinterpret_cast<const f32x4*>(nlse2 + qb * 32 + 16 * mb + 4 * g);
-            const f32x4 dv = *reinterpret_cast<const f32x4*>(ndel + qb * 32 + 16 * mb + 4 * g);
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                sa[mb][nb] = lv;
-                da[mb][nb] = dv;
-            }
-        }
-        if (kmask) {
-            const int key = wkey0 + (__builtin_amdgcn_mbcnt_lo(~0u, 0u) & 15);  // this lane's key (block nb = 0)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                const float kn = key + 16 * nb < S ? 0.f : -__builtin_inff();
-#pragma unroll
-                for (int mb = 0; mb < 2; ++mb) sa[mb][nb] += kn;
-            }
-        }
-#pragma unroll
-        for (int ks = 0; ks < D / 32; ++ks)
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb) {
-                const f16x8 qa = fo.rowop(Qs, qb * 32 + 16 * mb, ks), doa = fo.rowop(dOs, qb * 32 + 16 * mb, ks);
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    sa[mb][nb] = mfma16(qa, st.kf[nb][ks], sa[mb][nb]);
-                    da[mb][nb] = mfma16(doa, st.vf[nb][ks], da[mb][nb]);
-                }
-            }
-        f16x8 pf[2], dsf[2];  // [nb], k-slot j <-> query 16 (j >> 2) + 4g + (j & 3)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-                const float p0 = fast_exp2(sa[j >> 2][nb][j & 3]), p1 = fast_exp2(sa[j >> 2][nb][(j & 3) + 1]);
-                pf[nb][j] = to_tile(p0);
-                pf[nb][j + 1] = to_tile(p1);
-                const tile2 d2 = ds_pair(p0, p1, da[j >> 2][nb][j & 3], da[j >> 2][nb][(j & 3) + 1], pf[nb][j],
-                                         pf[nb][j + 1]);
-                dsf[nb][j] = d2[0];
-                dsf[nb][j + 1] = d2[1];
-            }
-        // dS into the dSᵀ image: k-slots 0..3 are queries qb*32 + 4g + 0..3, 4..7 are
-        // qb*32 + 16 + 4g + 0..3, of key row 16 nb + (l & 15)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            const i16x8 v = __builtin_bit_cast(i16x8, dsf[nb]);
-            *reinterpret_cast<i16x4*>(dsimg + oo.dsw[qb][0] + nb * 16 * 64) = __builtin_shufflevector(v, v, 0, 1, 2, 3);
-            *reinterpret_cast<i16x4*>(dsimg + oo.dsw[qb][1] + nb * 16 * 64) = __builtin_shufflevector(v, v, 4, 5, 6, 7);
-        }
-#pragma unroll
-        for (int md = 0; md < D / 16; ++md) {
-            const f16x8 a_do = fo.trop(dOs, qb * 32, md), a_q = fo.trop(Qs, qb * 32, md);
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                st.dva[md][nb] = mfma16(a_do, pf[nb], st.dva[md][nb]);
-                st.dka[md][nb] = mfma16(a_q, dsf[nb], st.dka[md][nb]);
-            }
-        }
-    }
-}
-
-// The wave's dQ part of one step: dQᵀ rows d of its D/32 16-blocks, columns its 16
-// queries, summed over the item's 256 keys.  A = Kᵀ (transposed reads of the K
-// image), B = dSᵀ (transposed reads of the step's image): both take a k-step's 32 keys
-// in the same packed order 16 (j >> 2) + 4g + (j & 3), so the sum is exact.  The K
-// image holds K·log2e/√D, so the part is scaled by ln 2 to dS·K/√D.
-template <int D>
-__device__ __forceinline__ void op_dq(f32x4 (&acc)[D / 32], const _Float16* kimg, const _Float16* dsimg,
-                                      const OpOffsets<D>& oo) {
-#pragma unroll
-    for (int m = 0; m < D / 32; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < OP_KEYS / 32; ++kk) {
-        const f16x8 b = cat4(lds_tr4(dsimg + oo.db[0] + kk * 32 * 64), lds_tr4(dsimg + oo.db[1] + kk * 32 * 64));
-#pragma unroll
-        for (int m = 0; m < D / 32; ++m)
-            acc[m] = mfma16(cat4(lds_tr4(kimg + oo.ka[m][0] + kk * 32 * D), lds_tr4(kimg + oo.ka[m][1] + kk * 32 * D)),
-                            b, acc[m]);
-    }
-#pragma unroll
-    for (int m = 0; m < D / 32; ++m) acc[m] *= 0.6931471805599453f;
-}
-
-// Δ = rowsum(dO ∘ O) of a staged step (one 8-float chunk per thread; the CPR threads of
-// a row are consecutive lanes): -Δ into the step's row-constant LDS, Δ to `out`.
-template <int D, int NT>
-__device__ __forceinline__ void op_delta(const TileStager<D, 64, NT>& a, const TileStager<D, 64, NT>& o, float* ndel,
-                                         float* __restrict__ out, int q0, int S, int tid) {
-    using TS = TileStager<D, 64, NT>;
-    static_assert(TS::CPT == 1, "one chunk per thread");
-    const f32x4 p0 = a.r[0][0] * o.r[0][0], p1 = a.r[0][1] * o.r[0][1];
-    float d = ((p0[0] + p0[1]) + (p0[2] + p0[3])) + ((p1[0] + p1[1]) + (p1[2] + p1[3]));
-#pragma unroll
-    for (int off = TS::CPR / 2; off > 0; off >>= 1) d += __shfl_xor(d, off);
-    const int row = tid / TS::CPR;
-    if ((TS::EXACT || tid < TS::CHUNKS) && tid % TS::CPR == 0) {
-        ndel[row] = -d;
-        if (out && q0 + row < S) out[q0 + row] = d;
-    }
-}
-
-template <int N>
-struct OpPar {
-    static constexpr int value = N;
-};
-
-template <int D>
-__global__ void __launch_bounds__(512)
-fa2_bwd_onepass_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                           const float* __restrict__ dO, const float* __restrict__ O, const float* __restrict__ LSE,
-                           float* __restrict__ Delta, float* __restrict__ dQ, float* __restrict__ dK,
-                           float* __restrict__ dV, int S, int BH, unsigned* __restrict__ ws) {
-    static_assert(D == 32 || D == 64, "one-pass backward: D <= 64");
-    using L = OpLds<D>;
-    constexpr int QT = L::QT, TILE = L::TILE, NT = 512, MD = D / 32;
-    __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
-    _Float16* const smem = reinterpret_cast<_Float16*>(lds);
-    _Float16* const kimg = smem + L::KI;
-    _Float16* const dsimg = smem + L::DSI;
-    float(*rows)[2][QT] = reinterpret_cast<float(*)[2][QT]>(lds + L::ROWS);
-    int* const slot = reinterpret_cast<int*>(lds + L::MISC);
-    float(*ostage)[32][36] = reinterpret_cast<float(*)[32][36]>(lds + 2 * L::DSI);  // epilogue: over the dS images
-
-    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nkb = (S + OP_KEYS - 1) / OP_KEYS, nqs = (S + QT - 1) / QT;
-    const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
-    int xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    xcc &= 7;
-
-    FragOffsets16<D> fo;
-    fo.init(lane);
-    OpOffsets<D> oo;
-    oo.init(lane, wave);
-    DkdvState16<D> st;
-    TileStager<D, QT, NT> qs, dos, os;
-
-    // next item (head * nkb + key block) or -1; the first call also reads the epoch
-    unsigned epoch = 0;
-    auto grab = [&](bool first) -> int {
-        __syncthreads();  // the previous item's LDS use is over
-        if (tid == 0) {
-            if (first) slot[1] = (int)op_ld(ws + OP_WS_EPOCH);
-            int got = -1;
-            for (int d = 0; d < 8 && got < 0; ++d) {
-                const int x = (xcc + d) & 7;
-                const unsigned nit = BH > x ? (unsigned)(((BH - 1 - x) / 8 + 1) * nkb) : 0u;
-                if (nit == 0 || op_ld(ws + x) >= nit) continue;
-                const unsigned i = op_add(ws + x, 1u);
-                if (i < nit) got = (x + 8 * (int)(i / nkb)) * nkb + (int)(i % nkb);
-            }
-            slot[0] = got;
-        }
-        __syncthreads();
-        if (first) epoch = (unsigned)__builtin_amdgcn_readfirstlane(slot[1]);
-        return __builtin_amdgcn_readfirstlane(slot[0]);
-    };
-
-    for (int item = grab(true); item >= 0; item = grab(false)) {
-        const int bh = item / nkb, kblk = item - bh * nkb;
-        const long base = (long)bh * S * D, rbase = (long)bh * S;
-        const int key0 = kblk * OP_KEYS, wkey0 = key0 + wave * 32;
-        const int off = (int)((long)kblk * nqs / nkb);
-        unsigned* const flags = ws + OP_WS_FLAGS + (long)bh * nqs * 8 + wave;  // + q * 8
-        const __amdgpu_buffer_rsrc_t rs_dq = head_rsrc(dQ + base, S, D);
-        const __amdgpu_buffer_rsrc_t rs_lse = head_rsrc(LSE + rbase, S, 1);
-        float* const dl_out = kblk == 0 ? Delta + rbase : nullptr;
-        const bool kmask = wkey0 + 32 > S;
-        auto qstep = [&](int t) {
-            const int q = t + off;
-            return q >= nqs ? q - nqs : q;
-        };
-        auto cpos = [&](int q) {  // chain position of this key block for query step q
-            const int p = ((q + 1) * nkb + nqs - 1) / nqs - 1 - kblk;
-            return p < 0 ? p + nkb : p;
-        };
-        float rowraw = 0.f;
-        int rowq = 0;
-        auto load_step = [&](int q0) {
-            qs.load(q0);
-            dos.load(q0);
-            os.load(q0);
-            if (wave == 0) {
-                rowq = q0 + lane;
-                rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_lse, lane * 4, q0 * 4, 0));
-            }
-        };
-        auto store_step = [&](int b, int q0) {
-            qs.store(smem + 2 * b * TILE, 1.f, tid);
-            dos.store(smem + (2 * b + 1) * TILE, 1.f, tid);
-            op_delta<D, NT>(dos, os, rows[b][1], dl_out, q0, S, tid);
-            if (wave == 0) rows[b][0][lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
-        };
-
-        // prologue: K (kept as the K image) and V (through dS image 1, first written in
-        // step 1) of the item, and the first step's Q, dO, O
-        {
-            TileStager<D, OP_KEYS, NT> kst, vst;
-            kst.init(K + base, S, tid);
-            vst.init(V + base, S, tid);
-            kst.load(key0);
-            vst.load(key0);
-            qs.init(Q + base, S, tid);
-            dos.init(dO + base, S, tid);
-            os.init(O + base, S, tid);
-            load_step(qstep(0) * QT);
-            kst.store(kimg, kscale, tid);
-            vst.store(dsimg + L::DSIMG, 1.f, tid);
-            store_step(0, qstep(0) * QT);
-            __syncthreads();
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int ks = 0; ks < D / 32; ++ks) {
-                    st.kf[nb][ks] = fo.rowop(kimg, wave * 32 + 16 * nb, ks);
-                    st.vf[nb][ks] = fo.rowop(dsimg + L::DSIMG, wave * 32 + 16 * nb, ks);
-                }
-#pragma unroll
-            for (int md = 0; md < D / 16; ++md)
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    st.dka[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    st.dva[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-                }
-        }
-
-        f32x4 part[MD], sum[MD];  // this wave's dQ part of the previous step; the chain's running sum
-        // The hand-off stores of a hop go out at the end of a step; their flag follows at
-        // the end of the NEXT step, behind a wait for all but that step's own hop stores
-        // (every older VMEM op, those stores included, is then done), so no drain sits
-        // on the critical path.
-        int pub_q = -1;
-        unsigned pub_v = 0;
-        auto publish = [&] {
-            if (pub_q >= 0) {
-                if constexpr (MD == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                if (lane == 0) op_st(flags + pub_q * 8, pub_v);
-            }
-        };
-        // the hop of a step's part: add the predecessor's sum (fetched at the step's
-        // start), then the final store (last position) or the write-through hand-off
-        auto hop = [&](int hq, int hpos) {
-            if (hpos > 0) {
-#pragma unroll
-                for (int m = 0; m < MD; ++m) part[m] += sum[m];
-            }
-            const int soff = hq * QT * D * 4;
-            if (hpos == nkb - 1) {
-#pragma unroll
-                for (int m = 0; m < MD; ++m)
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, part[m]), rs_dq, oo.voff[m], soff, 0);
-                return false;
-            }
-#pragma unroll
-            for (int m = 0; m < MD; ++m)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, part[m]), rs_dq, oo.voff[m], soff,
-                                                       16 /* sc1 */);
-            return true;
-        };
-        // the chain predecessor's running sum for step hq (its flag value polled as fv)
-        auto fetch = [&](int hq, int hpos, unsigned fv) {
-            const unsigned want = epoch * 64u + (unsigned)hpos;
-            const bool ok = fv == want || op_wait(flags + hq * 8, want, ws, epoch);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no load above the poll
-            const int soff = hq * QT * D * 4;
-#pragma unroll
-            for (int m = 0; m < MD; ++m)
-                sum[m] = ok ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_dq, oo.voff[m], soff, 16))
-                            : f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
-        };
-
-        // step t out of buffers b = t & 1, and the hop of step t - 1: the running sum is
-        // fetched at the step's start (flag polled one step ago, read into a scalar at that
-        // step's end, where the staging wait has already covered its load), the part is
-        // computed from dS image b ^ 1 at the step's end and handed on right away; the
-        // next step's loads go out between the query blocks.
-        int hpos_n = 0;
-        unsigned fv_n = 0;
-        auto step = [&](auto B_, int t) {
-            constexpr int b = decltype(B_)::value;
-            const bool more = t + 1 < nqs;
-            const int q1 = more ? qstep(t + 1) * QT : 0;
-            const int qt = qstep(t);
-            const int hq = t >= 1 ? qstep(t - 1) : 0, hpos = hpos_n;
-            if (t >= 1 && hpos > 0) fetch(hq, hpos, fv_n);
-            hpos_n = cpos(qt);
-            unsigned fv = 0;
-            if (hpos_n > 0) fv = op_ld(flags + qt * 8);
-            op_step<D>(st, smem + 2 * b * TILE, smem + (2 * b + 1) * TILE, rows[b][0], rows[b][1], fo, oo,
-                       dsimg + b * L::DSIMG, g, kmask, wkey0, S, [&] {
-                           if (more) load_step(q1);
-                       });
-            if (more) store_step(b ^ 1, q1);
-            // the flag into a scalar here, pinned before the hand-off stores: its load is
-            // older than the staging loads store_step has just waited for, so this costs no
-            // wait (sunk past the barrier, it cost a drain of those write-through stores)
-            fv_n = __builtin_amdgcn_readfirstlane(fv);
-            asm volatile("" ::"s"(fv_n));
-            bool handed = false;
-            if (t >= 1) {
-                op_dq<D>(part, kimg, dsimg + (b ^ 1) * L::DSIMG, oo);
-                handed = hop(hq, hpos);
-            }
-            publish();
-            pub_q = handed ? hq : -1;
-            pub_v = epoch * 64u + (unsigned)(hpos + 1);
-            __syncthreads();
-        };
-        for (int t = 0; t < nqs; t += 2) {
-            step(OpPar<0>{}, t);
-            if (t + 1 < nqs) step(OpPar<1>{}, t + 1);
-        }
-        // tail: the last step's hop (its part from the last dS image), the dK / dV epilogue
-        {
-            const int hq = qstep(nqs - 1), hpos = hpos_n;
-            if (hpos > 0) fetch(hq, hpos, fv_n);
-            if ((nqs - 1) & 1) op_dq<D>(part, kimg, dsimg + L::DSIMG, oo);
-            else op_dq<D>(part, kimg, dsimg, oo);
-            __syncthreads();  // every wave's dQ reads are done: the dS images take the stage
-            const float dscale = 1.f / __builtin_sqrtf((float)D);
-            store_block_rows16<D>(ostage[wave], st.dka, dscale, dK + base + (long)wkey0 * D, S - wkey0, lane);
-            store_block_rows16<D>(ostage[wave], st.dva, 1.f, dV + base + (long)wkey0 * D, S - wkey0, lane);
-            const bool handed = hop(hq, hpos);
-            publish();
-            if (handed) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) op_st(flags + hq * 8, epoch * 64u + (unsigned)(hpos + 1));
-            }
-        }
-    }
-    // leave: the last workgroup out rewinds the queues and advances the epoch
-    if (tid == 0 && op_add(ws + OP_WS_EXITED, 1u) == gridDim.x - 1) {
-#pragma unroll
-        for (int x = 0; x < 8; ++x) op_st(ws + x, 0u);
-        op_st(ws + OP_WS_EXITED, 0u);
-        op_st(ws + OP_WS_EPOCH, epoch + 1u);
-    }
-}
-
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
 // block 256, test_flash_attention2.py:499-535 / f-attn2-backward_f16.cu:445),
 // fp16 tiles on MFMA.  A workgroup owns 32 keys (B operands K*log2e/sqrt(D) and
@@ -2059,44 +1590,6 @@ hipError_t launch_bwd_fused_delta(int D, const float* q, const float* k, const f
 }
 }  // namespace
 
-namespace {
-template <int D>
-hipError_t onepass_launch(const float* q, const float* k, const float* v, const float* o, const float* dout,
-                          const float* lse, float* delta, float* dq, float* dk, float* dv, int bh, int S,
-                          hipStream_t stream) {
-    if constexpr (D > 64) {
-        return hipErrorNotSupported;
-    } else {
-        const int nkb = (S + fa2f16b::OP_KEYS - 1) / fa2f16b::OP_KEYS, nqs = (S + 63) / 64;
-        const long items = (long)bh * nkb;
-        const long ncu = cu_count();
-        const long grid = items < ncu ? items : ncu;
-        // deadlock guard (see the kernel): every item resident at once, or more workgroups
-        // than the 8 queues' partly handed-out heads can hold; flag values need nkb <= 64
-        if (nkb > 64 || items > 0x7fffffffL || (grid < items && 8L * (nkb - 1) >= grid)) return hipErrorNotSupported;
-        const size_t words = fa2f16b::OP_WS_FLAGS + (size_t)bh * nqs * 8;
-        unsigned* ws = static_cast<unsigned*>(bwd_workspace(stream, words * 4));
-        if (!ws) return hipErrorNotSupported;
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_onepass_f16_kernel<D>), dim3((unsigned)grid), dim3(512), 0, stream, q, k, v,
-                           dout, o, lse, delta, dq, dk, dv, S, bh, ws);
-        return hipGetLastError();
-    }
-}
-}  // namespace
-
-// dK, dV and dQ in one persistent launch (D <= 64), or hipErrorNotSupported where it
-// does not apply (D = 128, S > 16384, or too few CUs for the deadlock guard)
-hipError_t FA2_TILE_LAUNCH(launch_bwd_onepass)(int D, const float* q, const float* k, const float* v, const float* o,
-                                  const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
-                                  int bh, int S, hipStream_t stream) {
-    if (bh <= 0 || S <= 0) return hipErrorInvalidValue;
-    switch (D) {
-        case 32: return onepass_launch<32>(q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, stream);
-        case 64: return onepass_launch<64>(q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, stream);
-        default: return hipErrorNotSupported;
-    }
-}
-
 // Override BWD_FUSED (fa2_tune_set): 1 = Δ kernel, then dK/dV and dQ in one launch (D <= 64);
 // 0 = Δ fused into the dQ kernel's prologue (which stages dO anyway), then dK/dV,
 // which reads it; -1 (default) = 1 on grids of fewer than 8 blocks of 32 rows per
@@ -2105,17 +1598,6 @@ hipError_t FA2_TILE_LAUNCH(launch_bwd_onepass)(int D, const float* q, const floa
 hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream) {
-    // The one-pass launch only on request (override BWD_ONEPASS = 1, wherever it
-    // applies).  A/B in one process on one board (r02, fa2_backward, 7 rounds):
-    // C3 dO = ones 246.7 vs 234.1 us for the two kernels, dO ~ N(0,1) 257.4 vs 255.2;
-    // B16_H16_S2048 965 vs 952; B2_H8_S4096 222.5 vs 217.9 (ones), 238.0 vs 238.2
-    // (randn).  The two kernels recompute S and dP but need no cross-workgroup hand-off
-    // and re-read Q / dO / O from L2 far less (PMC: 0.4 vs 1.46 GB per C3 backward).
-    const int onepass = tune_knob("BWD_ONEPASS", 0);
-    if (D <= 64 && bh > 0 && S > 0 && onepass == 1) {
-        const hipError_t e = FA2_TILE_LAUNCH(launch_bwd_onepass)(D, q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, stream);
-        if (e != hipErrorNotSupported) return e;
-    }
     int fused = tune_knob("BWD_FUSED", -1);
     if (fused < 0) fused = bh > 0 && S > 0 && auto_waves((long)bh * ((S + 31) / 32), 8) < 8;
     if (D <= 64 && bh > 0 && S > 0 && fused == 1) {

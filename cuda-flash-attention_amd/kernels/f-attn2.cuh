@@ -119,23 +119,6 @@ hipError_t launch_bwd_dq_delta_bf16(int D, const float* q, const float* k, const
                                     const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
                                     hipStream_t stream);
 
-// dK, dV and dQ in ONE persistent launch (fp16 / bf16 tiles, D <= 64; what
-// launch_backward_* runs when the BWD_ONEPASS override is 1 -- by default it runs the
-// two kernels, measured faster), or hipErrorNotSupported where it does
-// not apply.  Uses bwd_workspace(stream).
-hipError_t launch_bwd_onepass_f16(int D, const float* q, const float* k, const float* v, const float* o,
-                                  const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
-                                  int bh, int S, hipStream_t stream);
-hipError_t launch_bwd_onepass_bf16(int D, const float* q, const float* k, const float* v, const float* o,
-                                   const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
-                                   int bh, int S, hipStream_t stream);
-
-// Device workspace of the one-pass backward: at least `bytes`, zeroed when allocated,
-// cached per (device, stream) and reused across calls (its words carry a call epoch,
-// so nothing is cleared per call).  nullptr where none can be had without allocating
-// during a graph capture.  release_workspace frees a stream's (before the stream goes).
-void* bwd_workspace(hipStream_t stream, size_t bytes);
-void release_workspace(hipStream_t stream);
 // compute units of the current device (cached)
 int cu_count();
 

@@ -229,15 +229,6 @@ struct TileStager {
             r[c][1] = buf_load4(rs, voff[c] + 16, soff);
         }
     }
-    // one chunk (c < CPT) of load / store, for callers that spread them out
-    __device__ __forceinline__ void load_c(int c, int row0) {
-        const int soff = row0 * D * 4;
-        r[c][0] = buf_load4(rs, voff[c], soff);
-        r[c][1] = buf_load4(rs, voff[c] + 16, soff);
-    }
-    __device__ __forceinline__ void store_c(int c, _Float16* tile, float scale, int tid) const {
-        if (EXACT || tid + c * NT < CHUNKS) *reinterpret_cast<f16x8*>(tile + loff[c]) = to_f16x8(r[c][0], r[c][1], scale);
-    }
     __device__ __forceinline__ void store(_Float16* tile, float scale, int tid) const {
         if (!on) return;
 #pragma unroll
@@ -647,418 +638,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     }
 }
 
-// ---------------------------------------------------------------------------
-// forward, two-chain ping-pong (full grids)
-// ---------------------------------------------------------------------------
-// One wave per SIMD (4-wave workgroups of 256 query rows, up to 512 registers per
-// lane), 64 query rows per wave as two 32-row chains A and B.  A wave alone on its
-// SIMD gets no help from a partner wave, so it overlaps its own work: while the
-// matrix pipe runs one chain's MFMAs, the vector pipe runs the other chain's
-// softmax.  Per 64-key tile j (guide Appendix B, the 4-wave structure):
-//
-//   R1(j):  O_B += V(j-1)·P_B(j-1),  S_B(j) = K(j)·Q_Bᵀ   ||  P_A(j) = exp2(S_A(j))
-//   ---- barrier ----
-//   R2(j):  O_A += V(j)·P_A(j),      S_A(j+1) = K(j+1)·Q_Aᵀ ||  P_B(j) = exp2(S_B(j)),
-//           stage K(j+2), V(j+1) into LDS, load K(j+3), V(j+2) into registers
-//
-// Between two barriers the workgroup reads exactly {K(j+1), V(j)}, so one barrier
-// per tile and two LDS slots per tensor suffice: the slots of K(j) and V(j-1) are
-// free in that window and take K(j+2) and V(j+1).  The order inside each region is
-// fixed by sched_group_barrier (one MFMA, then its share of exponentials, other
-// VALU and LDS reads), the regions fenced by sched_barrier.
-//
-// Softmax as in fa2_fwd_f16_kernel (lazy reference max, fp16-range guard): the
-// guard's branch sits at the end of each region, where the chain's S tile is still
-// live and its P·V not yet issued.  Row sums are f32 adds (guide: v_dot2c beside
-// MFMAs costs ~10 cycles beyond its issue slot).
-template <int D>
-struct PPChain {
-    f32x16 o[D / 32];
-    f32x16 nm;  // -m, the initial value of the chain's S^T accumulators
-    float m;
-    float l[2];
-};
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-// P of one chain and tile, as packed fp16 pairs: w[kb][s][k] = keys 8s + 2k, +1 of
-// the lane's 16 in 32-key block kb (the f16x8 B operand of P·V is w[kb][s][0..3])
-struct PPTile {
-    unsigned w[2][2][4];
-    __device__ __forceinline__ f16x8 op(int kb, int s) const {
-        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 v = {w[kb][s][0], w[kb][s][1], w[kb][s][2], w[kb][s][3]};
-        return __builtin_bit_cast(f16x8, v);
-    }
-};
-
-// keys >= S of the ragged last tile -> -inf
-__device__ __forceinline__ void pp_mask(f32x16 (&s)[2], int k0, int S, int h) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            if (k0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h >= S) s[kb][i] = -__builtin_inff();
-}
-
-__device__ __forceinline__ unsigned pp_pack(float a, float b) {
-#ifdef FA2_TILE_BF16
-    const f16x2 v = {to_tile(a), to_tile(b)};
-#else
-    const f16x2 v = __builtin_convertvector(f32x2{a, b}, f16x2);
-#endif
-    return __builtin_bit_cast(unsigned, v);
-}
-
-// score pair e, e + 1 (e even) of a chain's tile: p = exp2(s - sh), packed, summed
-template <bool SHIFT>
-__device__ __forceinline__ void pp_pair(const f32x16 (&s)[2], float sh, PPTile& p, float (&ls)[2], int e) {
-    const int kb = e >> 4, r = e & 15;
-    const float p0 = fast_exp2(SHIFT ? s[kb][r] - sh : s[kb][r]);
-    const float p1 = fast_exp2(SHIFT ? s[kb][r + 1] - sh : s[kb][r + 1]);
-    p.w[kb][r >> 3][(r & 7) >> 1] = pp_pack(p0, p1);
-    if (e == 0) {
-        ls[0] = p0;
-        ls[1] = p1;
-    } else {
-        ls[0] += p0;
-        ls[1] += p1;
-    }
-}
-
-// slow path: the tile's row max moves m (first tile: m := row max), l and O rescale,
-// and P is recomputed against the new m
-template <int D, bool FIRST>
-__device__ __forceinline__ void pp_fix(PPChain<D>& c, const f32x16 (&s)[2], PPTile& p, float (&ls)[2]) {
-    const float mx = xor32_max(tile_max<2>(s));
-    const float d = FIRST ? mx : fmaxf(mx, 0.f);
-    c.m += d;
-    if (!FIRST) {
-        const float alpha = fast_exp2(-d);
-        c.l[0] *= alpha;
-        c.l[1] *= alpha;
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) c.o[b][i] *= alpha;
-    }
-    c.nm = splat16(-c.m);
-#pragma unroll
-    for (int e = 0; e < 32; e += 2) pp_pair<true>(s, d, p, ls, e);
-}
-
-// One region of the ping-pong loop, issued in a fixed order: NS MFMA slots (the PV
-// MFMAs of chain X against V, then X's QK^T MFMAs against K and X's Q rows, both
-// 32-key blocks per Q fragment), each slot followed by its share of chain Y's
-// softmax (NE exponentials, packing, row-sum adds), the LDS reads of the slot LEAD
-// ahead, and a piece of the tile staging.  Slots are fenced by sched_barrier, so
-// source order is issue order (the IGroupLP solver left every MFMA of such a region
-// first).
-template <int V>
-struct PPC {
-    static constexpr int value = V;
-};
-
-#ifndef FA2_PP_LEAD
-#define FA2_PP_LEAD 2  // LDS reads issued this many MFMA slots ahead of their MFMA
-#endif
-template <int D, bool PV, bool QK, bool SM, int STG>
-__device__ __forceinline__ void pp_region(PPChain<D>& X, const PPTile& pX, const _Float16* Vs, f32x16 (&sX)[2],
-                                          const _Float16* Ks, const _Float16* Qx, const f32x16 (&sY)[2], PPTile& pY,
-                                          float (&lsY)[2], const FragOffsets<D>& fo, TileStager<D, 64, 256>& stg,
-                                          _Float16* stg_dst, int stg_row, int tid) {
-    constexpr int NB = D / 32, NT16 = D / 16;
-    constexpr int NPV = PV ? 4 * NB : 0, NQK = QK ? 2 * NT16 : 0;
-    constexpr int NS = NPV + NQK;
-    constexpr int LEAD = FA2_PP_LEAD;
-    constexpr int NE = SM ? 32 / NS : 0;  // exponentials per slot
-    static_assert(!SM || NE * NS == 32, "softmax share");
-    f16x8 fr[NS], qfr[NT16];
-    float pe[8];  // exponentials in flight (two slots' worth)
-    // pack and sum the exponential pairs [e0, e1)
-    auto pp_finish = [&](int e0, int e1) {
-#pragma unroll
-        for (int e = e0; e < e1; e += 2) {
-            const float p0 = pe[e & 7], p1 = pe[(e + 1) & 7];
-            const int kb = e >> 4, r = e & 15;
-            pY.w[kb][r >> 3][(r & 7) >> 1] = pp_pack(p0, p1);
-            asm volatile("" : "+v"(pY.w[kb][r >> 3][(r & 7) >> 1]));
-#ifdef FA2_PP_DOT2
-            const float c = e == 0 ? 0.f : lsY[(e >> 1) & 1];
-            lsY[(e >> 1) & 1] = pair_sum(__builtin_bit_cast(f16x2, pY.w[kb][r >> 3][(r & 7) >> 1])[0],
-                                         __builtin_bit_cast(f16x2, pY.w[kb][r >> 3][(r & 7) >> 1])[1], c);
-            if (e == 0) lsY[1] = 0.f;
-#elif defined(FA2_PP_ABL_NOSUM)  // timing-only ablation
-            if (e == 0) {
-                lsY[0] = p0;
-                lsY[1] = p1;
-            }
-#else
-            if (e == 0) {
-                lsY[0] = p0;
-                lsY[1] = p1;
-            } else {
-                lsY[0] += p0;
-                lsY[1] += p1;
-            }
-#endif
-        }
-    };
-    auto fetch = [&](int i) {
-#ifdef FA2_PP_ABL_NOLDS  // timing-only ablation: one read per operand kind
-        if (i > 1 && i < NPV) { fr[i] = fr[i & 1]; return; }
-        if (i >= NPV + 2) { fr[i] = fr[NPV + (i & 1)]; if (((i - NPV) & 1) == 0) qfr[(i - NPV) >> 1] = qfr[0]; return; }
-#endif
-        if (i < NPV) {
-            const int kb = i / (2 * NB), s = (i / NB) & 1, b = i % NB;
-            fr[i] = fo.trop(Vs, kb * 32 + 16 * s, b);
-        } else {
-            const int q = i - NPV, t = q >> 1, kb = q & 1;
-            if (kb == 0) qfr[t] = fo.rowop(Qx, 0, t);
-            fr[i] = fo.rowop(Ks, kb * 32, t);
-        }
-    };
-#pragma unroll
-    for (int i = 0; i < LEAD && i < NS; ++i) fetch(i);
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        if (i + LEAD < NS) fetch(i + LEAD);
-        if (i < NPV) {
-            const int kb = i / (2 * NB), s = (i / NB) & 1, b = i % NB;
-            X.o[b] = mfma(fr[i], pX.op(kb, s), X.o[b]);
-        } else {
-            const int q = i - NPV, t = q >> 1, kb = q & 1;
-            sX[kb] = mfma(fr[i], qfr[t], t == 0 ? X.nm : sX[kb]);
-        }
-        if (SM) {
-            // this slot's exponentials, then the packing and sums of the previous
-            // slot's (one slot later, so neither waits on a fresh v_exp result)
-#pragma unroll
-            for (int e = i * NE; e < (i + 1) * NE; ++e) {
-#ifdef FA2_PP_ABL_NOEXP  // timing-only ablation
-                pe[e & 7] = sY[e >> 4][e & 15];
-#else
-                pe[e & 7] = fast_exp2(sY[e >> 4][e & 15]);
-#endif
-                asm volatile("" : "+v"(pe[e & 7]));
-            }
-            if (i > 0) pp_finish(((i - 1) * NE) & ~1, (i * NE) & ~1);  // pairs issued before slot i
-        }
-        // staging of the next K or V tile (2 chunks of 8 floats per thread): LDS stores
-        // of the registers loaded one iteration ago, then the loads for the next one
-        if (STG) {
-            constexpr int Q4 = NS / 8 > 0 ? NS / 8 : 1;
-            if (i == 1 * Q4) stg.store_c(0, stg_dst, 1.f, tid);
-            if (i == 3 * Q4) stg.store_c(1, stg_dst, 1.f, tid);
-            if (i == 5 * Q4) stg.load_c(0, stg_row);
-            if (i == 7 * Q4 || (NS < 8 && i == NS - 1)) stg.load_c(1, stg_row);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if (SM) pp_finish(((NS - 1) * NE) & ~1, 32);
-}
-
-// Diagnostic build only (-DFA2_PP_STAMPS, never shipped): s_memtime per loop segment,
-// summed per wave into a buffer of its own (read by tools/pp_stamps.py); read the
-// SHARES, not the lengths (guide §7, In-kernel stamps).
-#ifdef FA2_PP_STAMPS
-__device__ unsigned long long fa2_pp_stamps[1 << 16];
-#define PP_STAMP(t)                                                                      \
-    do {                                                                                 \
-        __builtin_amdgcn_sched_barrier(0);                                               \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");       \
-        __builtin_amdgcn_sched_barrier(0);                                               \
-    } while (0)
-#else
-#define PP_STAMP(t) ((void)0)
-#endif
-
-template <int D>
-__global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(1, 1)))
-fa2_fwd_pp_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                  float* __restrict__ O, float* __restrict__ LSE, int S) {
-    constexpr int KT = 64, TILE = KT * D, NT = 256, QB = 256;
-    // [K slot 0 | K slot 1 | V slot 0 | V slot 1 | Q block (256 rows, 4 tiles)]
-    __shared__ __attribute__((aligned(16))) _Float16 smem[8 * TILE];
-    __shared__ __attribute__((aligned(16))) float ostage[4][32][36];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-    const int nqb = (S + QB - 1) / QB;
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = bid / nqb, qb = bid - bh * nqb;
-    const long base = (long)bh * S * D;
-    const int nt = (S + KT - 1) / KT;
-#ifdef FA2_PP_STAMPS
-    unsigned long long sacc_[8] = {}, ta_, tb_, tk0_;
-    PP_STAMP(tk0_);
-#endif
-    _Float16* const qblk = smem + 4 * TILE;
-    const _Float16* const qA = qblk + wave * 64 * D;  // chain A's 32 rows, B's follow
-    const _Float16* const qB = qA + 32 * D;
-
-    FragOffsets<D> fo;
-    fo.init(lane);
-    TileStager<D, KT, NT> ks, vs;
-    ks.init(K + base, S, tid);
-    vs.init(V + base, S, tid);
-    PPChain<D> A, B;
-    // prologue: Q block -> LDS (scaled fp16, read back per tile); K(0), V(0), K(1) ->
-    // LDS; K(2) -> staging registers (stored in R2(0)).  V(j) is stored in R1(j)
-    // (j >= 1) and K(j+2) in R2(j): each goes into the slot its predecessor two tiles
-    // back left, which no wave reads between the two barriers around it.
-    {
-        TileStager<D, QB, NT> qst;
-        qst.init(Q + base, S, tid);
-        qst.load(qb * QB);
-        ks.load(0);
-        vs.load(0);
-        qst.store(qblk, FA2_LOG2E / __builtin_sqrtf((float)D), tid);
-        ks.store(smem, 1.f, tid);
-        vs.store(smem + 2 * TILE, 1.f, tid);
-        ks.load(KT);
-        ks.store(smem + TILE, 1.f, tid);
-        ks.load(2 * KT);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-#pragma unroll
-    for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) A.o[b][i] = B.o[b][i] = 0.f;
-    A.m = B.m = 0.f;
-    A.nm = splat16(0.f);
-    B.nm = splat16(0.f);
-    A.l[0] = A.l[1] = B.l[0] = B.l[1] = 0.f;
-
-    f32x16 sA[2], sB[2];
-    PPTile pA, pB;
-    float lsA[2], lsB[2];
-    pp_region<D, false, true, false, 0>(A, pA, nullptr, sA, smem, qA, sB, pB, lsB, fo, vs, nullptr, 0, tid);  // S_A(0)
-
-    // tile j; PAR = j & 1 (K(j), V(j) live in slot PAR)
-    auto iter = [&](auto first_t, auto last_t, auto mask_t, auto par_t, int j) {
-        constexpr bool FIRST = decltype(first_t)::value != 0, LAST = decltype(last_t)::value != 0;
-        constexpr bool MASK = decltype(mask_t)::value != 0;
-        constexpr int PAR = decltype(par_t)::value;
-        _Float16* const Kc = smem + PAR * TILE;        // K(j); K(j+2) goes here in R2(j)
-        _Float16* const Kn = smem + (1 - PAR) * TILE;  // K(j+1)
-        _Float16* const Vc = smem + (2 + PAR) * TILE;  // V(j), stored in R1(j)
-        _Float16* const Vp = smem + (3 - PAR) * TILE;  // V(j-1)
-#ifdef FA2_PP_STAMPS
-        PP_STAMP(ta_);
-#endif
-        // ---- R1(j): O_B += V(j-1) P_B(j-1), S_B(j) = K(j) Q_B^T || P_A(j); stage V(j)
-        if (MASK) pp_mask(sA, j * KT, S, h);
-        if (FIRST) {
-            pp_region<D, false, true, false, 2>(B, pB, Vp, sB, Kc, qB, sA, pA, lsA, fo, vs, Vc, (j + 1) * KT, tid);
-            pp_fix<D, true>(A, sA, pA, lsA);
-        } else {
-            pp_region<D, true, true, true, 1>(B, pB, Vp, sB, Kc, qB, sA, pA, lsA, fo, vs, Vc, (j + 1) * KT, tid);
-#ifdef FA2_PP_STAMPS
-            PP_STAMP(tb_);
-            sacc_[0] += tb_ - ta_;
-            ta_ = tb_;
-#endif
-            if (__any(!(lsA[0] + lsA[1] <= FA2_TILE_SUM_MAX))) pp_fix<D, false>(A, sA, pA, lsA);
-        }
-        A.l[0] += lsA[0];
-        A.l[1] += lsA[1];
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#ifdef FA2_PP_STAMPS
-        PP_STAMP(tb_);
-        sacc_[1] += tb_ - ta_;
-        ta_ = tb_;
-#endif
-        // ---- R2(j): O_A += V(j) P_A(j), S_A(j+1) = K(j+1) Q_A^T || P_B(j); stage K(j+2)
-        if (MASK) pp_mask(sB, j * KT, S, h);
-        if (FIRST) {
-            pp_region<D, true, !LAST, false, LAST ? 0 : 1>(A, pA, Vc, sA, Kn, qA, sB, pB, lsB, fo, ks, Kc,
-                                                          (j + 3) * KT, tid);
-            pp_fix<D, true>(B, sB, pB, lsB);
-        } else {
-            pp_region<D, true, !LAST, true, LAST ? 0 : 1>(A, pA, Vc, sA, Kn, qA, sB, pB, lsB, fo, ks, Kc,
-                                                         (j + 3) * KT, tid);
-#ifdef FA2_PP_STAMPS
-            PP_STAMP(tb_);
-            sacc_[2] += tb_ - ta_;
-            ta_ = tb_;
-#endif
-            if (__any(!(lsB[0] + lsB[1] <= FA2_TILE_SUM_MAX))) pp_fix<D, false>(B, sB, pB, lsB);
-        }
-        B.l[0] += lsB[0];
-        B.l[1] += lsB[1];
-        // (no barrier here: between the barrier above and the next tile's the
-        // workgroup reads only K(j+1) and V(j), and writes only the other two slots)
-#ifdef FA2_PP_STAMPS
-        PP_STAMP(tb_);
-        sacc_[3] += tb_ - ta_;
-        sacc_[6] += 1;
-#endif
-    };
-#ifdef FA2_PP_STAMPS
-    PP_STAMP(ta_);
-    sacc_[4] = ta_ - tk0_;
-#endif
-    using T = PPC<1>;
-    using F = PPC<0>;
-    using P0 = PPC<0>;
-    using P1 = PPC<1>;
-    const bool ragged = (S % KT) != 0;
-    if (nt == 1) {
-        if (ragged) iter(T{}, T{}, T{}, P0{}, 0);
-        else iter(T{}, T{}, F{}, P0{}, 0);
-    } else {
-        iter(T{}, F{}, F{}, P0{}, 0);
-        int j = 1;
-        for (; j + 2 < nt; j += 2) {
-            iter(F{}, F{}, F{}, P1{}, j);
-            iter(F{}, F{}, F{}, P0{}, j + 1);
-        }
-        if (j + 1 < nt) {  // j odd: one more full tile before the last
-            iter(F{}, F{}, F{}, P1{}, j);
-            ++j;
-        }
-        if (j & 1) {  // j = nt - 1
-            if (ragged) iter(F{}, T{}, T{}, P1{}, j);
-            else iter(F{}, T{}, F{}, P1{}, j);
-        } else {
-            if (ragged) iter(F{}, T{}, T{}, P0{}, j);
-            else iter(F{}, T{}, F{}, P0{}, j);
-        }
-    }
-    // O_B += V(nt-1) P_B(nt-1)
-    pp_region<D, true, false, false, 0>(B, pB, smem + (2 + ((nt - 1) & 1)) * TILE, sB, nullptr, nullptr, sA, pA, lsA,
-                                        fo, vs, nullptr, 0, tid);
-
-    // epilogue: O through a wave-private LDS stage, whole 128-B row segments
-    float(*os)[36] = ostage[wave];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const PPChain<D>& ch = c ? B : A;
-        const float lt = xor32_sum(ch.l[0] + ch.l[1]);
-        const float inv = 1.f / lt;
-        const int qrow0 = qb * QB + wave * 64 + 32 * c;
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) os[r][(i & 3) + 8 * (i >> 2) + 4 * h] = ch.o[b][i] * inv;
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const int row = 8 * s4 + (lane >> 3), c4 = (lane & 7) * 4;
-                const f32x4 v = *reinterpret_cast<const f32x4*>(&os[row][c4]);
-                if (qrow0 + row < S) *reinterpret_cast<f32x4*>(O + base + (long)(qrow0 + row) * D + 32 * b + c4) = v;
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (h == 0 && qrow0 + r < S) LSE[(long)bh * S + qrow0 + r] = ch.m * FA2_LN2 + __logf(lt);
-    }
-#ifdef FA2_PP_STAMPS
-    PP_STAMP(tb_);
-    sacc_[5] = tb_ - tk0_;
-    if (lane == 0 && blockIdx.x * 4 + wave < (1 << 13))
-        for (int k = 0; k < 8; ++k) fa2_pp_stamps[(blockIdx.x * 4 + wave) * 8 + k] = sacc_[k];
-#endif
-}
-
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
 // block 256, test_flash_attention2.py:278-281 / kernel_fa2_optimized_f16.cu:401),
 // fp16 tiles on MFMA like the library kernel.  A workgroup owns 32 query rows;
@@ -1147,20 +726,8 @@ static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v,
 }
 
 template <int D>
-static hipError_t fwd_pp_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
-                                hipStream_t stream) {
-    const long grid = (long)bh * ((S + 255) / 256);
-    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_pp_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, o, lse, S);
-    return hipGetLastError();
-}
-
-template <int D>
 static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
                                    hipStream_t stream) {
-    // two-chain ping-pong kernel (FWD_PP: 1 forces it, 0 never)
-    if constexpr (D >= 64)
-        if (tune_knob("FWD_PP", 0) == 1) return fwd_pp_launch<D>(q, k, v, o, lse, bh, S, stream);
     // 8 waves (2 per SIMD) where the registers allow it; D = 128 runs 4 waves of
     // ~400 VGPRs (8 would spill and exceed the LDS budget with the Q stages)
     // (MQ = 2, two 32-row query groups per wave at 4 waves / 1 per SIMD, measured
@@ -1202,12 +769,6 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     if (nw == 2) return fwd_f16_launch<D, 2>(q, k, v, o, lse, bh, S, stream);
     return fwd_f16_launch<D, 4>(q, k, v, o, lse, bh, S, stream);
 }
-
-#if defined(FA2_PP_STAMPS) && !defined(FA2_TILE_BF16)
-extern "C" int fa2_debug_pp_stamps(unsigned long long* out, int n) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(fa2f16::fa2_pp_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
-}
-#endif
 
 hipError_t FA2_TILE_LAUNCH(launch_forward)(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,
                               int S, hipStream_t stream) {

@@ -76,8 +76,7 @@ int fa2_backward_dq(const float* q, const float* k, const float* v, const float*
  * what fa2_backward runs for FA2_FP16 / FA2_BF16 on grids of at least 8 blocks of 32
  * rows per CU and at D = 128; on smaller grids (D <= 64) it runs ONE launch whose
  * workgroups take the dK/dV or the dQ role side by side (BWD_FUSED; Δ computed inside
- * it below 4 blocks per CU, else fa2_delta first).  BWD_ONEPASS = 1 selects the
- * one-pass persistent kernel instead (D <= 64). */
+ * it below 4 blocks per CU, else fa2_delta first). */
 int fa2_backward_dq_delta(const float* q, const float* k, const float* v, const float* o, const float* dout,
                           const float* lse, float* delta, float* dq, int batch, int heads, int seq, int head_dim,
                           void* stream);
@@ -118,11 +117,15 @@ int fa2_shard_range(int total_heads, int shards, int index, int* first, int* cou
 /* Launch-plan override (tests and tuning tools only; nothing is read from the
  * environment).  fa2_tune_set("DKDV_QS", 2) makes the next launches use that plan
  * where the shape allows it; fa2_tune_set(NULL, 0) clears every override.  Knobs:
- * FWD_WAVES, FWD_KS, DKDV_WAVES, DKDV_QS, DQ_WAVES, DQ_KS, BWD_FUSED, BWD_FQS,
- * BWD_FKS, BWD_FNW, BWD_ONEPASS (see the launchers in kernels/), and the test-only
- * HOST_SHARDS_ON_DEVICE0 = 1 (fa2_*_host run every shard on device 0, so an N-way
- * split's head offsets are testable on one GPU).  Process-wide. */
+ * FWD_WAVES, FWD_KS, DKDV_WAVES, DKDV_QS, DQ_WAVES, DQ_KS, BWD_FUSED,
+ * BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW (see the launchers in kernels/), and
+ * the test-only HOST_SHARDS_ON_DEVICE0 = 1 (fa2_*_host run every shard on device 0,
+ * so an N-way split's head offsets are testable on one GPU).  Any other name:
+ * FA2_E_INVALID.  Process-wide.
+ * fa2_tune_get: 1 and *value when `knob` is overridden, 0 when it is not,
+ * FA2_E_INVALID for an unknown name. */
 int fa2_tune_set(const char* knob, int value);
+int fa2_tune_get(const char* knob, int* value);
 
 const char* fa2_last_error(void);
 int fa2_version(void); /* MAJOR*10000 + MINOR*100 + PATCH */

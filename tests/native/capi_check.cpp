@@ -103,25 +103,32 @@ static void tune_table() {
     CHECK(fa2::tune_knob("FWD_WAVES", -5) == -5);
     CHECK(fa2_tune_set("", 1) == FA2_E_INVALID);
     CHECK(fa2_tune_set("A_NAME_LONGER_THAN_THIRTY_TWO_CHARS", 1) == FA2_E_INVALID);
+    CHECK(fa2_tune_set("FWD_WAVE", 4) == FA2_E_INVALID);  // misspelt: rejected, not stored
+    CHECK(fa2::tune_knob("FWD_WAVE", -1) == -1);
+    int v = -7;
+    CHECK(fa2_tune_get("FWD_WAVES", &v) == 0 && v == -7);
+    CHECK(fa2_tune_get("NOT_A_KNOB", &v) == FA2_E_INVALID);
     CHECK(fa2_tune_set("FWD_WAVES", 4) == FA2_OK);
     CHECK(fa2_tune_set("FWD_WAVES", 8) == FA2_OK);  // overwrite, not append
     CHECK(fa2::tune_knob("FWD_WAVES", 0) == 8);
-    // concurrent writers (distinct knobs, the table grows) and readers
+    CHECK(fa2_tune_get("FWD_WAVES", &v) == 1 && v == 8);
+    // concurrent writers (every knob, the table grows) and readers
+    static const char* const names[] = {"FWD_KS", "DKDV_WAVES", "DKDV_QS", "DQ_WAVES", "DQ_KS", "BWD_FUSED",
+                                        "BWD_FQS", "BWD_FKS"};
     std::vector<std::thread> th;
     for (int t = 0; t < 4; ++t)
         th.emplace_back([t] {
-            char name[32];
             for (int i = 0; i < 200; ++i) {
-                std::snprintf(name, sizeof name, "K%d_%d", t, i % 50);
-                fa2_tune_set(name, i);
+                fa2_tune_set(names[(2 * t + i) % 8], i);
                 (void)fa2::tune_knob("FWD_WAVES", 0);
             }
         });
     for (auto& x : th) x.join();
-    CHECK(fa2::tune_knob("K3_49", -1) == 199);
     CHECK(fa2::tune_knob("FWD_WAVES", 0) == 8);
+    CHECK(fa2::tune_knob("BWD_FKS", -1) >= 0);
     CHECK(fa2_tune_set(nullptr, 0) == FA2_OK);
-    CHECK(fa2::tune_knob("K3_49", -1) == -1);
+    CHECK(fa2::tune_knob("BWD_FKS", -1) == -1);
+    CHECK(fa2_tune_get("FWD_WAVES", &v) == 0);
 }
 
 // host API with more devices than visible: a code, no exit, nothing leaked

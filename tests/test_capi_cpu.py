@@ -33,7 +33,28 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version():
-    assert fa2amd.version() == 10100
+    assert fa2amd.version() == 10200
+
+
+def test_tune_overrides_validated_and_restored():
+    """fa2_tune_set rejects names outside the documented knob list (a misspelt knob
+    would otherwise leave an A/B on the default plan), and fa2amd.tuned restores the
+    overrides that were set before the block, nested blocks included."""
+    fa2amd.tune_set(None)
+    with pytest.raises(fa2amd.FA2Error, match="unknown knob"):
+        fa2amd.tune_set("FWD_WAVE", 4)
+    with pytest.raises(fa2amd.FA2Error, match="unknown knob"):
+        fa2amd.tune_get("NOPE")
+    assert all(fa2amd.tune_get(k) is None for k in fa2amd.KNOBS)
+    fa2amd.tune_set("DQ_KS", 2)
+    with fa2amd.tuned(DKDV_QS=2, DQ_KS=4):
+        assert fa2amd.tune_get("DKDV_QS") == 2 and fa2amd.tune_get("DQ_KS") == 4
+        with fa2amd.tuned(FWD_WAVES=4):
+            assert fa2amd.tune_get("FWD_WAVES") == 4 and fa2amd.tune_get("DKDV_QS") == 2
+        assert fa2amd.tune_get("FWD_WAVES") is None and fa2amd.tune_get("DQ_KS") == 4
+    assert fa2amd.tune_get("DQ_KS") == 2 and fa2amd.tune_get("DKDV_QS") is None
+    fa2amd.tune_set(None)
+    assert fa2amd.tune_get("DQ_KS") is None
 
 
 def test_invalid_arguments_rejected_without_device():

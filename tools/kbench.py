@@ -68,7 +68,7 @@ def main():
                          fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
                          fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv)),
         "dqd": lambda: fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
-        # fwd + fa2_backward (whatever launch plan launch_backward picks, e.g. BWD_ONEPASS)
+        # fwd + fa2_backward (whatever launch plan launch_backward picks, e.g. BWD_FUSED)
         "stepb": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
                           fa2amd.backward(q, k, v, o, do, lse, "fp16", dq=dq, dk=dk, dv=dv, delta_buf=dl)),
         # dK/dV and dQ on two streams after a separate delta kernel
