@@ -23,8 +23,10 @@ value = algorithmic fwd+bwd FLOPs of the job (14*B*H*S^2*D) / the max over ranks
 the K-step wall time (barrier + synchronize on both sides).
 roofline = the dominant kernel launch's algorithmic FLOPs / its mean duration, timed
 live with HIP events on the launch's own stream around every launch of a second
-K-step region, against the dense fp16 MFMA peak; traffic = its HBM bytes per launch
-from the committed rocprofv3 PMC summary (profiles/pmc_summary.json).
+K-step region, against the dense fp16 MFMA peak; step_frac = the whole step's
+algorithmic rate (value) against the same peak; traffic = the dominant launch's HBM
+bytes from the committed rocprofv3 PMC summary (profiles/pmc_summary.json), null
+unless that profile was taken of this very build (fa2_build_id).
 cpu_baseline (rank 0, N = 1) = PyTorch-CPU SDPA fwd+bwd (north_star's baseline) on
 the host's usable cores, 2 warm-ups then the median of >= 3 runs, on whole heads of
 the workload; the harness's compute_reference and the C restatement of the oracle
@@ -68,18 +70,23 @@ def log(*a):
 PMC_PREFIX = {"fwd": "fa2_fwd_f16", "dq": "fa2_bwd_dq_f16", "dkdv": "fa2_bwd_dkdv_f16", "bwd32": "fa2_bwd_f32"}
 
 
-def traffic_from_profile(kernel: str, D: int, S: int, heads: int):
+def traffic_from_profile(kernel: str, D: int, S: int, heads: int, build_id: str, path: str | None = None):
     """HBM bytes per launch of `kernel` (FETCH_SIZE x 2 + WRITE_SIZE, gfx950-corrected)
     from the committed rocprofv3 PMC summary profiles/pmc_summary.json (tools/pmc.sh ->
-    tools/pmc_summary.py), or None when it does not cover this kernel and shape."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    tools/pmc_summary.py), or None when it does not cover this kernel and shape, or was
+    taken of another build than the loaded library (its _meta.build_id against
+    fa2_build_id(): a rebuilt kernel never inherits an old traffic figure)."""
+    path = path or os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             summ = json.load(f)
     except (OSError, ValueError):
         return None
     meta = summ.get("_meta", {})
-    if meta and (meta.get("S") != S or meta.get("D") != D or meta.get("heads") != heads):
+    if meta.get("S") != S or meta.get("D") != D or meta.get("heads") != heads:
+        return None
+    if meta.get("build_id") != build_id:
+        log(f"profiles/pmc_summary.json is of build {meta.get('build_id')}, the library is {build_id}: traffic null")
         return None
     for name, ent in summ.items():
         if name.startswith(PMC_PREFIX.get(kernel, "?")) and (f"<{D}," in name or f"<{D}>" in name):
@@ -487,9 +494,11 @@ def main():
     dom_flops = alg[dom] * per_head * heads
     peak = MFMA_F16_PEAK_TFLOPS if prec in ("fp16", "bf16") else MFMA_F32_PEAK_TFLOPS
     achieved = dom_flops / (kms[dom] * 1e-3) / 1e12
-    traffic = traffic_from_profile(dom if prec != "fp32" else "bwd32", D, S, heads)
+    traffic = traffic_from_profile(dom if prec != "fp32" else "bwd32", D, S, heads, fa2amd.build_id())
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,
+            # the whole step against the same peak: 14 S^2 D per head per step / ms_per_step
+            "step_frac": round(tflops / peak, 4),
             "kernel_ms": {n: round(x, 4) for n, x in kms.items()},
             "bwd_tflops": round(10.0 * per_head * heads / (sum(kms[n] for n in kms if n != "fwd") * 1e-3) / 1e12, 2),
             "ms_per_step_with_events": round(elapsed_ev / args.steps * 1e3, 4)}

@@ -116,6 +116,11 @@ extern "C" {
 
 int fa2_version(void) { return 1 * 10000 + 2 * 100 + 0; }
 
+#ifndef FA2_BUILD_ID
+#define FA2_BUILD_ID "unknown"
+#endif
+const char* fa2_build_id(void) { return FA2_BUILD_ID; }
+
 int fa2_tune_set(const char* knob, int value) {
     if (knob && !known_knob(knob)) return fail(FA2_E_INVALID, "unknown knob name");
     std::lock_guard<std::mutex> lock(g_tune_mu);

@@ -35,7 +35,7 @@ C_SYMBOLS = (
     "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv", "fa2_backward_dq", "fa2_backward_dq_delta",
     "fa2_naive_forward", "fa2_fa1_forward",
     "fa2_forward_host", "fa2_backward_host", "fa2_shard_range", "fa2_tune_set", "fa2_tune_get", "fa2_last_error",
-    "fa2_version", "fa2_device_count",
+    "fa2_version", "fa2_build_id", "fa2_device_count",
 )
 # launch-plan overrides fa2_tune_set accepts (include/fa2_amd.h)
 KNOBS = ("FWD_WAVES", "FWD_KS", "DKDV_WAVES", "DKDV_QS", "DQ_WAVES", "DQ_KS", "BWD_FUSED", "BWD_FUSED_DELTA",
@@ -100,6 +100,7 @@ def _load(path):
         "fa2_tune_get": [ctypes.c_char_p, ctypes.POINTER(I)],
         "fa2_last_error": [],
         "fa2_version": [],
+        "fa2_build_id": [],
         "fa2_device_count": [],
     }
     for name, args in sig.items():
@@ -107,7 +108,7 @@ def _load(path):
             continue  # an older build A/B'd by tools/kbench.py may lack newer entry points
         fn = getattr(L, name)
         fn.argtypes = args
-        fn.restype = ctypes.c_char_p if name == "fa2_last_error" else I
+        fn.restype = ctypes.c_char_p if name in ("fa2_last_error", "fa2_build_id") else I
     return L
 
 
@@ -118,6 +119,12 @@ def _check(rc: int):
 
 def version() -> int:
     return lib().fa2_version()
+
+
+def build_id() -> str:
+    """Hash of the sources and flags the loaded library was built from."""
+    L = lib()
+    return L.fa2_build_id().decode() if hasattr(L, "fa2_build_id") else "unknown"
 
 
 def tune_set(knob, value: int = 0):

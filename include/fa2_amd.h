@@ -129,6 +129,9 @@ int fa2_tune_get(const char* knob, int* value);
 
 const char* fa2_last_error(void);
 int fa2_version(void); /* MAJOR*10000 + MINOR*100 + PATCH */
+/* Hash of the sources and flags this library was built from (16 hex digits):
+ * profiles that depend on the kernels' code (rocprofv3 PMC traffic) record it. */
+const char* fa2_build_id(void);
 int fa2_device_count(void);
 
 #ifdef __cplusplus

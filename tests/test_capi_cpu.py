@@ -265,3 +265,26 @@ def test_experiment_seqlen_plot(monkeypatch, tmp_path):
         assert (tmp_path / f).stat().st_size > 0, f
     lines = (tmp_path / "experiment_results.csv").read_text().splitlines()
     assert sorted({int(ln.split(",")[5]) for ln in lines[1:]}) == list(experiments.SEQLEN_SWEEP)
+
+
+def test_bench_traffic_only_from_a_profile_of_the_loaded_build(tmp_path):
+    """roofline.traffic comes from profiles/pmc_summary.json only when its _meta.build_id
+    is the loaded library's fa2_build_id (a rebuilt kernel cannot inherit old figures)."""
+    import json
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    bid = fa2amd.build_id()
+    assert len(bid) == 16 and bid != "unknown"
+    summ = {"_meta": {"S": 2048, "D": 64, "heads": 64, "build_id": bid},
+            "fa2_bwd_dkdv_f16_kernel<64,8,1,true,1>": {"hbm_bytes_per_launch": 123.0}}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps(summ))
+    assert bench.traffic_from_profile("dkdv", 64, 2048, 64, bid, str(p)) == 123.0
+    assert bench.traffic_from_profile("dkdv", 64, 2048, 64, "0" * 16, str(p)) is None
+    assert bench.traffic_from_profile("dkdv", 64, 4096, 64, bid, str(p)) is None
+    summ["_meta"].pop("build_id")
+    p.write_text(json.dumps(summ))
+    assert bench.traffic_from_profile("dkdv", 64, 2048, 64, bid, str(p)) is None

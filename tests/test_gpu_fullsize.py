@@ -8,8 +8,9 @@ star's, un-scaled: 1e-2 for fp16 tiles (bf16 tiles, an extension, 2e-2).
 
   C3  B4_H16_S2048_D64   fp16 fwd+bwd   every one of the 64 heads
   C4  B8_H16_S4096_D128  fp16 fwd       every one of the 128 heads; a 4-head bwd at the same S, D
-  C5  B64_H16_S2048_D64  fp16 fwd+bwd   one GPU (1024 heads): 32 heads spread over the tensor
-                                        against the oracle, identities on every head; and the
+  C5  B64_H16_S2048_D64  fp16 fwd+bwd   one GPU (1024 heads): 158 heads against the oracle
+                                        (one whole 8-way shard, 128 heads, and 32 spread over
+                                        the tensor), identities on every head; and the
                                         north star's 8-way B*H split through fa2_*_host, every
                                         shard on device 0 (HOST_SHARDS_ON_DEVICE0), so the
                                         non-zero shard offsets of capi.cpp run_shard execute
@@ -156,10 +157,12 @@ def test_c4_shape_backward_heads():
 # C5: B64_H16_S2048_D64 on one GPU, and as the north star's 8-way B*H split
 # ---------------------------------------------------------------------------
 C5 = (64, 16, 2048, 64)
-# 32 heads spread over the tensor, including both ends and every 8-way shard's first
-# and last head (shards of 128 heads)
+# 158 heads: one whole 8-way shard (heads 640..767, shard 5 of fa2_shard_range) and 32
+# heads spread over the tensor, including both ends and every shard's first and last
+# head (shards of 128 heads)
+C5_SHARD = list(range(5 * 128, 6 * 128))
 C5_SAMPLE = sorted({0, 1, 1023} | {s * 128 for s in range(8)} | {s * 128 + 127 for s in range(8)}
-                   | {37 + 71 * i for i in range(14)})
+                   | {37 + 71 * i for i in range(14)} | set(C5_SHARD))
 
 
 @pytest.fixture(scope="module")

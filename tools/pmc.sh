@@ -21,5 +21,8 @@ for p in "${PASSES[@]}"; do
   echo "pass $i rc=$rc" >> $OUT/status.txt
   [ $rc -ne 0 ] && exit $rc
 done
-PMC_META='{"S": 2048, "D": 64, "heads": 64, "workload": "B4_H16_S2048_D64 fp16, bench.py --steps 5 --warmup 2", "source": "tools/pmc.sh"}' python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1
+# the build id of the library the passes profiled: bench.py reports traffic only while
+# the library it loads has the same one (a rebuilt kernel cannot inherit old figures)
+BID=$(python3 -c "import sys; sys.path.insert(0, 'cuda-flash-attention_amd'); import fa2amd; print(fa2amd.build_id())")
+PMC_META='{"S": 2048, "D": 64, "heads": 64, "workload": "B4_H16_S2048_D64 fp16, bench.py --steps 5 --warmup 2", "source": "tools/pmc.sh", "build_id": "'$BID'"}' python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1
 echo done >> $OUT/status.txt
