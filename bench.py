@@ -294,29 +294,36 @@ def extras(fa2amd, torch, dev):
     return out
 
 
-def host_api_entry(fa2amd, B, H, S, D, runs=3):
+def host_api_entry(fa2amd, B, H, S, D, runs=3, num_devices=1):
     """The reference's host-buffer boundary (host_flash_attention2_{forward,backward}_fp16
-    semantics through fa2_{forward,backward}_host): per call device alloc, H2D, kernels,
-    D2H, free.  Wall time of fwd + bwd from host arrays (PCIe-inclusive; reported beside
-    the HBM-resident `value`, never as it) and the kernel-only ms the calls report."""
+    semantics through fa2_{forward,backward}_host): H2D, kernels, D2H per call, the
+    heads sharded over `num_devices` GPUs.  Wall time of fwd + bwd from host arrays
+    (PCIe-inclusive; reported beside the HBM-resident `value`, never as it) and the
+    kernel-only ms the calls report.  The result arrays are allocated once and reused,
+    as a caller looping over batches does (fresh ones add the page faults of their
+    first touch to every call)."""
     gen = np.random.default_rng(3)
     q, k, v = (gen.random((B, H, S, D), dtype=np.float32) for _ in range(3))
     do = np.ones_like(q)
+    o, lse = np.empty_like(q), np.empty((B, H, S), np.float32)
+    dq, dk, dv = np.empty_like(q), np.empty_like(q), np.empty_like(q)
     walls, kms = [], []
     for i in range(runs + 1):
         t0 = time.perf_counter()
-        o, lse, kf = fa2amd.forward_host(q, k, v, "fp16")
-        _, _, _, kb = fa2amd.backward_host(q, k, v, o, do, lse, "fp16")
-        if i:  # the first call pays the device-allocator warm-up
+        _, _, kf = fa2amd.forward_host(q, k, v, "fp16", num_devices=num_devices, out=o, lse=lse)
+        _, _, _, kb = fa2amd.backward_host(q, k, v, o, do, lse, "fp16", num_devices=num_devices, dq=dq, dk=dk, dv=dv)
+        if i:  # the first call pays the device scratch allocation and the first touch
             walls.append(time.perf_counter() - t0)
             kms.append(kf + kb)
+    fa2amd.host_release()
     wall, km = statistics.median(walls), statistics.median(kms)
     flops = 14.0 * B * H * S * S * D
+    nbytes = 4 * B * H * S * D * (3 + 1 + 5 + 3) + 4 * B * H * S * 2
     return {"wall_ms": round(wall * 1e3, 3), "tflops_wall": round(flops / wall / 1e12, 2), "kernel_ms": round(km, 4),
-            "tflops_kernels": round(flops / (km * 1e-3) / 1e12, 2),
-            "h2d_d2h_bytes": 4 * B * H * S * D * (3 + 1 + 5 + 3) + 4 * B * H * S * 2,
-            "what": "fa2_forward_host + fa2_backward_host from host numpy buffers (alloc, H2D, kernels, D2H, free "
-                    "per call), median of 3"}
+            "tflops_kernels": round(flops / (km * 1e-3) / 1e12, 2), "h2d_d2h_bytes": nbytes,
+            "pcie_gbps": round(nbytes / wall / 1e9, 1), "num_devices": num_devices,
+            "what": f"fa2_forward_host + fa2_backward_host from host numpy buffers, B*H over {num_devices} device(s) "
+                    f"(H2D, kernels, D2H per call; result arrays reused), median of {runs}"}
 
 
 # ---------------------------------------------------------------------------
@@ -509,6 +516,15 @@ def main():
         extra = extras(fa2amd, torch, dev)
     elif world > 1 and not args.no_extras:
         extra = {f"sweep_B2_H8_D64_fp16_fwdbwd_sharded{world}": sweep_sharded(fa2amd, torch, dev, dist, world, rank)}
+        # the reference's host-buffer semantics at the N-GPU point: rank 0 shards C5 over
+        # all N devices through fa2_*_host (one host thread per device) while the other
+        # ranks wait at the barrier (rehearsals on one GPU skip it)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        if rank == 0 and not rehearse:
+            Bc, Hc, Sc, Dc, _ = WORKLOADS["c5"]
+            extra["c5_host_api_pcie_inclusive"] = host_api_entry(fa2amd, Bc, Hc, Sc, Dc, runs=2, num_devices=world)
+        dist.barrier()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(S, D, 16)

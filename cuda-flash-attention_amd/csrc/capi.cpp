@@ -53,14 +53,6 @@ int check_precision(int precision) {
     return FA2_OK;
 }
 
-// RAII device buffer
-struct DevBuf {
-    float* p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-};
-
 }  // namespace
 
 namespace {
@@ -73,7 +65,7 @@ std::atomic<int> g_tune_n{0};
 // so a misspelt knob cannot silently leave an A/B on the default plan)
 const char* const kKnobs[] = {"FWD_WAVES", "FWD_KS",    "DKDV_WAVES", "DKDV_QS", "DQ_WAVES",        "DQ_KS",
                               "BWD_FUSED", "BWD_FUSED_DELTA", "BWD_FQS", "BWD_FKS", "BWD_FNW",
-                              "HOST_SHARDS_ON_DEVICE0"};
+                              "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS"};
 bool known_knob(const char* k) {
     for (const char* n : kKnobs)
         if (!strcmp(n, k)) return true;
@@ -252,77 +244,197 @@ struct HostJob {
     // host tensors (full) and this shard's head range
     const float* in[6] = {};  // q k v o dout lse
     float* out[5] = {};       // o lse | dq dk dv
-    int heads0 = 0, nheads = 0, S = 0, D = 0, precision = 0, device = 0;
+    int heads0 = 0, nheads = 0, S = 0, D = 0, precision = 0, device = 0, pool = 0;
     bool backward = false;
     float ms = 0.f;
     int rc = FA2_OK;
     std::string err;
 };
 
+// Device scratch of the host-pointer API, kept between calls (grow-only) instead of a
+// hipMalloc / hipFree per tensor per call: the allocations and frees cost more than
+// the kernels at C3.  One pool per (device, shard slot); a call holds its pool's lock
+// for its duration.  fa2_host_release() frees them.
+struct DevPool {
+    std::mutex mu;
+    int device = -1;
+    void* p = nullptr;
+    size_t bytes = 0;
+    // streams (compute, H2D, D2H) and events of the pipeline, made once per pool:
+    // creating them per call cost ~10 ms of a 15 ms C3 forward call
+    int sdev = -1;
+    hipStream_t sc = nullptr, si = nullptr, so = nullptr;
+    std::vector<hipEvent_t> ev;
+    void drop_streams() {
+        for (auto e : ev) (void)hipEventDestroy(e);
+        ev.clear();
+        for (hipStream_t* s : {&sc, &si, &so})
+            if (*s) (void)hipStreamDestroy(*s), *s = nullptr;
+        sdev = -1;
+    }
+};
+constexpr int kPools = 64;
+DevPool g_pools[kPools];
+
+int pool_acquire(DevPool& pl, int device, size_t bytes, char** base) {
+    if (pl.p && (pl.bytes < bytes || pl.device != device)) {
+        const int prev = pl.device;
+        (void)hipSetDevice(prev);
+        (void)hipFree(pl.p);
+        (void)hipSetDevice(device);
+        pl.p = nullptr;
+        pl.bytes = 0;
+    }
+    if (!pl.p) {
+        int rc;
+        if ((rc = hip_status(hipMalloc(&pl.p, bytes), "hipMalloc"))) return rc;
+        pl.bytes = bytes;
+        pl.device = device;
+    }
+    *base = static_cast<char*>(pl.p);
+    return FA2_OK;
+}
+
+// One shard on one device, as a head-chunked pipeline: H2D of chunk c+1 (this
+// thread) overlaps the kernels of chunk c (compute stream) and the D2H of chunk c-1
+// (a second host thread: PCIe is full duplex, and a copy from or to pageable memory
+// occupies its calling thread).  *ms = the sum of the chunks' kernel times.
 int run_shard(HostJob& j) {
-    const size_t row = (size_t)j.S * j.D;             // floats per head, [S][D]
-    const size_t n = (size_t)j.nheads * row;          // floats per tensor in this shard
-    const size_t nl = (size_t)j.nheads * j.S;         // floats per [heads][S] vector
+    const size_t row = (size_t)j.S * j.D;  // floats per head, [S][D]
+    const size_t n = (size_t)j.nheads * row, nl = (size_t)j.nheads * j.S;
     const size_t off = (size_t)j.heads0 * row, offl = (size_t)j.heads0 * j.S;
     if (hipSetDevice(j.device) != hipSuccess) return fail(FA2_E_DEVICE, "hipSetDevice failed");
+    // tensors: forward q k v | o lse; backward q k v o dout lse | delta dq dk dv
+    const int nin = j.backward ? 6 : 3, nout = j.backward ? 3 : 2;
+    const int ntens = j.backward ? 10 : 5;
+    auto is_vec = [&](int t) { return j.backward ? (t == 5 || t == 6) : t == 4; };
+    size_t bytes = 0;
+    size_t toff[10];
+    for (int t = 0; t < ntens; ++t) {
+        toff[t] = bytes;
+        bytes += ((is_vec(t) ? nl : n) * 4 + 255) & ~size_t(255);
+    }
+    DevPool& pl = g_pools[j.pool % kPools];
+    std::lock_guard<std::mutex> lock(pl.mu);
+    char* base = nullptr;
     int rc;
-    hipStream_t st = nullptr;
-    if ((rc = hip_status(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate"))) return rc;
-    struct StreamGuard {
-        hipStream_t s;
-        ~StreamGuard() { (void)hipStreamDestroy(s); }
-    } sg{st};
-    hipEvent_t e0, e1;
-    if ((rc = hip_status(hipEventCreate(&e0), "hipEventCreate"))) return rc;
-    if ((rc = hip_status(hipEventCreate(&e1), "hipEventCreate"))) {
-        (void)hipEventDestroy(e0);
-        return rc;
-    }
-    struct EventGuard {
-        hipEvent_t a, b;
-        ~EventGuard() {
-            (void)hipEventDestroy(a);
-            (void)hipEventDestroy(b);
-        }
-    } eg{e0, e1};
+    if ((rc = pool_acquire(pl, j.device, bytes, &base))) return rc;
+    auto dptr = [&](int t) { return reinterpret_cast<float*>(base + toff[t]); };
+    // host side of tensor t: inputs then outputs
+    auto hin = [&](int t) { return j.in[t]; };
+    auto hout = [&](int t) { return j.backward ? j.out[2 + t] : j.out[t]; };
+    // device tensor of output t
+    auto dout_t = [&](int t) { return j.backward ? dptr(7 + t) : dptr(3 + t); };
+    auto out_vec = [&](int t) { return !j.backward && t == 1; };
 
-    if (!j.backward) {
-        DevBuf q, k, v, o, l;
-        if ((rc = hip_status(hipMalloc(&q.p, n * 4), "hipMalloc")) || (rc = hip_status(hipMalloc(&k.p, n * 4), "hipMalloc")) ||
-            (rc = hip_status(hipMalloc(&v.p, n * 4), "hipMalloc")) || (rc = hip_status(hipMalloc(&o.p, n * 4), "hipMalloc")) ||
-            (rc = hip_status(hipMalloc(&l.p, nl * 4), "hipMalloc")))
+    // chunks of heads: about 16 MB of each [S][D] tensor per chunk, at most 4
+    int nch = (int)std::min<size_t>(4, std::max<size_t>(1, n * 4 / (size_t(16) << 20)));
+    if (const int f = fa2::tune_knob("HOST_CHUNKS", 0)) nch = f;  // A/B override
+    nch = std::max(1, std::min(nch, j.nheads));
+    if (pl.sdev != j.device) {
+        if (pl.sdev >= 0) {
+            (void)hipSetDevice(pl.sdev);
+            pl.drop_streams();
+            (void)hipSetDevice(j.device);
+        }
+        if ((rc = hip_status(hipStreamCreateWithFlags(&pl.sc, hipStreamNonBlocking), "hipStreamCreate")) ||
+            (rc = hip_status(hipStreamCreateWithFlags(&pl.si, hipStreamNonBlocking), "hipStreamCreate")) ||
+            (rc = hip_status(hipStreamCreateWithFlags(&pl.so, hipStreamNonBlocking), "hipStreamCreate"))) {
+            pl.drop_streams();
             return rc;
-        if ((rc = hip_status(hipMemcpy(q.p, j.in[0] + off, n * 4, hipMemcpyHostToDevice), "H2D")) ||
-            (rc = hip_status(hipMemcpy(k.p, j.in[1] + off, n * 4, hipMemcpyHostToDevice), "H2D")) ||
-            (rc = hip_status(hipMemcpy(v.p, j.in[2] + off, n * 4, hipMemcpyHostToDevice), "H2D")))
-            return rc;
-        (void)hipEventRecord(e0, st);
-        rc = fa2_forward(q.p, k.p, v.p, o.p, l.p, 1, j.nheads, j.S, j.D, j.precision, st);
-        if (rc) return rc;
-        (void)hipEventRecord(e1, st);
-        if ((rc = hip_status(hipEventSynchronize(e1), "kernel"))) return rc;
-        (void)hipEventElapsedTime(&j.ms, e0, e1);
-        if ((rc = hip_status(hipMemcpy(j.out[0] + off, o.p, n * 4, hipMemcpyDeviceToHost), "D2H")) ||
-            (rc = hip_status(hipMemcpy(j.out[1] + offl, l.p, nl * 4, hipMemcpyDeviceToHost), "D2H")))
-            return rc;
-        return FA2_OK;
+        }
+        pl.sdev = j.device;
     }
-    DevBuf t[10];  // q k v o dout lse delta dq dk dv
-    const size_t sz[10] = {n, n, n, n, n, nl, nl, n, n, n};
-    for (int i = 0; i < 10; ++i)
-        if ((rc = hip_status(hipMalloc(&t[i].p, sz[i] * 4), "hipMalloc"))) return rc;
-    for (int i = 0; i < 6; ++i)
-        if ((rc = hip_status(hipMemcpy(t[i].p, j.in[i] + (i == 5 ? offl : off), sz[i] * 4, hipMemcpyHostToDevice), "H2D")))
-            return rc;
-    (void)hipEventRecord(e0, st);
-    rc = fa2_backward(t[0].p, t[1].p, t[2].p, t[3].p, t[4].p, t[5].p, t[6].p, t[7].p, t[8].p, t[9].p, 1, j.nheads,
-                      j.S, j.D, j.precision, st);
-    if (rc) return rc;
-    (void)hipEventRecord(e1, st);
-    if ((rc = hip_status(hipEventSynchronize(e1), "kernel"))) return rc;
-    (void)hipEventElapsedTime(&j.ms, e0, e1);
-    for (int i = 0; i < 3; ++i)
-        if ((rc = hip_status(hipMemcpy(j.out[2 + i] + off, t[7 + i].p, n * 4, hipMemcpyDeviceToHost), "D2H"))) return rc;
+    while ((int)pl.ev.size() < 3 * nch) {  // [c]: inputs in, kernels start, kernels end
+        hipEvent_t e = nullptr;
+        if ((rc = hip_status(hipEventCreate(&e), "hipEventCreate"))) return rc;
+        pl.ev.push_back(e);
+    }
+    DevPool& r = pl;
+    std::vector<int> h0(nch + 1);
+    for (int c = 0; c <= nch; ++c) h0[c] = (int)((long)j.nheads * c / nch);
+
+    // D2H thread: waits for each chunk's kernels, copies its outputs back
+    std::atomic<int> issued{0};  // chunks whose kernels are enqueued
+    std::atomic<bool> abort{false};
+    int out_rc = FA2_OK;
+    std::string out_err;
+    std::thread d2h([&] {
+        if (hipSetDevice(j.device) != hipSuccess) {
+            out_rc = fail(FA2_E_DEVICE, "hipSetDevice failed");
+            out_err = g_err;
+            return;
+        }
+        for (int c = 0; c < nch; ++c) {
+            while (issued.load(std::memory_order_acquire) <= c && !abort.load(std::memory_order_acquire))
+                std::this_thread::yield();
+            if (abort.load(std::memory_order_acquire)) return;
+            int e;
+            if ((e = hip_status(hipStreamWaitEvent(r.so, r.ev[3 * c + 2], 0), "hipStreamWaitEvent"))) {
+                out_rc = e;
+                out_err = g_err;
+                return;
+            }
+            const size_t hc = h0[c + 1] - h0[c];
+            for (int t = 0; t < nout; ++t) {
+                const size_t per = out_vec(t) ? (size_t)j.S : row;
+                const size_t ho = (out_vec(t) ? offl : off) + h0[c] * per;
+                if ((e = hip_status(hipMemcpyAsync(hout(t) + ho, dout_t(t) + h0[c] * per, hc * per * 4,
+                                                   hipMemcpyDeviceToHost, r.so),
+                                    "D2H"))) {
+                    out_rc = e;
+                    out_err = g_err;
+                    return;
+                }
+            }
+        }
+        if (int e = hip_status(hipStreamSynchronize(r.so), "D2H")) {
+            out_rc = e;
+            out_err = g_err;
+        }
+    });
+    auto stop = [&](int code) {
+        abort.store(true, std::memory_order_release);
+        d2h.join();
+        return code;
+    };
+    for (int c = 0; c < nch; ++c) {
+        const int hc = h0[c + 1] - h0[c];
+        for (int t = 0; t < nin; ++t) {
+            const bool v = j.backward && t == 5;
+            const size_t per = v ? (size_t)j.S : row;
+            const size_t ho = (v ? offl : off) + h0[c] * per;
+            if ((rc = hip_status(hipMemcpyAsync(dptr(t) + h0[c] * per, hin(t) + ho, hc * per * 4, hipMemcpyHostToDevice,
+                                                r.si),
+                                 "H2D")))
+                return stop(rc);
+        }
+        if ((rc = hip_status(hipEventRecord(r.ev[3 * c], r.si), "hipEventRecord")) ||
+            (rc = hip_status(hipStreamWaitEvent(r.sc, r.ev[3 * c], 0), "hipStreamWaitEvent")) ||
+            (rc = hip_status(hipEventRecord(r.ev[3 * c + 1], r.sc), "hipEventRecord")))
+            return stop(rc);
+        const size_t cr = h0[c] * row, cl = (size_t)h0[c] * j.S;
+        if (!j.backward)
+            rc = fa2_forward(dptr(0) + cr, dptr(1) + cr, dptr(2) + cr, dptr(3) + cr, dptr(4) + cl, 1, hc, j.S, j.D,
+                             j.precision, r.sc);
+        else
+            rc = fa2_backward(dptr(0) + cr, dptr(1) + cr, dptr(2) + cr, dptr(3) + cr, dptr(4) + cr, dptr(5) + cl,
+                              dptr(6) + cl, dptr(7) + cr, dptr(8) + cr, dptr(9) + cr, 1, hc, j.S, j.D, j.precision,
+                              r.sc);
+        if (rc) return stop(rc);
+        if ((rc = hip_status(hipEventRecord(r.ev[3 * c + 2], r.sc), "hipEventRecord"))) return stop(rc);
+        issued.store(c + 1, std::memory_order_release);
+    }
+    d2h.join();
+    if (out_rc) return fail(out_rc, out_err);
+    if ((rc = hip_status(hipStreamSynchronize(r.sc), "kernel"))) return rc;
+    float ms = 0.f;
+    for (int c = 0; c < nch; ++c) {
+        float x = 0.f;
+        (void)hipEventElapsedTime(&x, r.ev[3 * c + 1], r.ev[3 * c + 2]);
+        ms += x;
+    }
+    j.ms = ms;
     return FA2_OK;
 }
 
@@ -340,6 +452,7 @@ int run_sharded(HostJob proto, int B, int H, int num_devices, float* kernel_ms) 
     for (int g = 0; g < ndev; ++g) {
         fa2_shard_range(total, ndev, g, &jobs[g].heads0, &jobs[g].nheads);
         jobs[g].device = one_device ? 0 : g;
+        jobs[g].pool = g;
     }
     auto body = [](HostJob* j) {
         j->rc = run_shard(*j);
@@ -364,6 +477,26 @@ int run_sharded(HostJob proto, int B, int H, int num_devices, float* kernel_ms) 
 }  // namespace
 
 extern "C" {
+
+int fa2_host_release(void) {
+    int dev0 = 0;
+    const bool have = hipGetDevice(&dev0) == hipSuccess;
+    for (auto& pl : g_pools) {
+        std::lock_guard<std::mutex> lock(pl.mu);
+        if (pl.sdev >= 0) {
+            (void)hipSetDevice(pl.sdev);
+            pl.drop_streams();
+        }
+        if (pl.p) {
+            (void)hipSetDevice(pl.device);
+            (void)hipFree(pl.p);
+            pl.p = nullptr;
+            pl.bytes = 0;
+        }
+    }
+    if (have) (void)hipSetDevice(dev0);
+    return FA2_OK;
+}
 
 int fa2_forward_host(const float* q, const float* k, const float* v, float* o, float* lse, int B, int H, int S, int D,
                      int precision, int num_devices, float* kernel_ms) {

@@ -34,12 +34,12 @@ SUPPORTED_HEAD_DIMS = (32, 64, 128)
 C_SYMBOLS = (
     "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv", "fa2_backward_dq", "fa2_backward_dq_delta",
     "fa2_naive_forward", "fa2_fa1_forward",
-    "fa2_forward_host", "fa2_backward_host", "fa2_shard_range", "fa2_tune_set", "fa2_tune_get", "fa2_last_error",
+    "fa2_forward_host", "fa2_backward_host", "fa2_host_release", "fa2_shard_range", "fa2_tune_set", "fa2_tune_get", "fa2_last_error",
     "fa2_version", "fa2_build_id", "fa2_device_count",
 )
 # launch-plan overrides fa2_tune_set accepts (include/fa2_amd.h)
 KNOBS = ("FWD_WAVES", "FWD_KS", "DKDV_WAVES", "DKDV_QS", "DQ_WAVES", "DQ_KS", "BWD_FUSED", "BWD_FUSED_DELTA",
-         "BWD_FQS", "BWD_FKS", "BWD_FNW", "HOST_SHARDS_ON_DEVICE0")
+         "BWD_FQS", "BWD_FKS", "BWD_FNW", "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS")
 
 
 class FA2Error(RuntimeError):
@@ -95,6 +95,7 @@ def _load(path):
         "fa2_fa1_forward": [P] * 6 + [I] * 4 + [V],
         "fa2_forward_host": [P] * 5 + [I] * 6 + [FP],
         "fa2_backward_host": [P] * 9 + [I] * 6 + [FP],
+        "fa2_host_release": [],
         "fa2_shard_range": [I, I, I, ctypes.POINTER(I), ctypes.POINTER(I)],
         "fa2_tune_set": [ctypes.c_char_p, I],
         "fa2_tune_get": [ctypes.c_char_p, ctypes.POINTER(I)],
@@ -356,28 +357,39 @@ def _host_shape(q):
     return q.shape
 
 
-def forward_host(q, k, v, precision="fp32", num_devices=1):
-    """(O, LSE, kernel_ms) from host arrays: host_flash_attention2_forward[_fp16] semantics."""
+def forward_host(q, k, v, precision="fp32", num_devices=1, out=None, lse=None):
+    """(O, LSE, kernel_ms) from host arrays: host_flash_attention2_forward[_fp16] semantics.
+    ``out`` / ``lse``: caller-owned result arrays (reused, as a caller looping over
+    batches would; fresh ones are allocated otherwise)."""
     import numpy as np
 
     B, H, S, D = _host_shape(q)
-    o = np.empty_like(q)
-    lse = np.empty((B, H, S), np.float32)
+    o = np.empty_like(q) if out is None else out
+    lse = np.empty((B, H, S), np.float32) if lse is None else lse
     ms = ctypes.c_float(0.0)
-    _check(lib().fa2_forward_host(_np(q, "q"), _np(k, "k", q.shape), _np(v, "v", q.shape), _np(o, "o"), _np(lse, "lse"),
-                                  B, H, S, D, _PRECISION[precision], num_devices, ctypes.byref(ms)))
+    _check(lib().fa2_forward_host(_np(q, "q"), _np(k, "k", q.shape), _np(v, "v", q.shape), _np(o, "o", q.shape),
+                                  _np(lse, "lse", (B, H, S)), B, H, S, D, _PRECISION[precision], num_devices,
+                                  ctypes.byref(ms)))
     return o, lse, ms.value
 
 
-def backward_host(q, k, v, o, dout, lse, precision="fp32", num_devices=1):
-    """(dQ, dK, dV, kernel_ms) from host arrays: host_flash_attention2_backward[_fp16] semantics."""
+def backward_host(q, k, v, o, dout, lse, precision="fp32", num_devices=1, dq=None, dk=None, dv=None):
+    """(dQ, dK, dV, kernel_ms) from host arrays: host_flash_attention2_backward[_fp16]
+    semantics (``dq`` / ``dk`` / ``dv``: caller-owned result arrays, optional)."""
     import numpy as np
 
     B, H, S, D = _host_shape(q)
-    dq, dk, dv = np.empty_like(q), np.empty_like(q), np.empty_like(q)
+    dq = np.empty_like(q) if dq is None else dq
+    dk = np.empty_like(q) if dk is None else dk
+    dv = np.empty_like(q) if dv is None else dv
     ms = ctypes.c_float(0.0)
     _check(lib().fa2_backward_host(_np(q, "q"), _np(k, "k", q.shape), _np(v, "v", q.shape), _np(o, "o", q.shape),
-                                   _np(dout, "dout", q.shape), _np(lse, "lse", (B, H, S)), _np(dq, "dq"), _np(dk, "dk"),
-                                   _np(dv, "dv"),
+                                   _np(dout, "dout", q.shape), _np(lse, "lse", (B, H, S)), _np(dq, "dq", q.shape),
+                                   _np(dk, "dk", q.shape), _np(dv, "dv", q.shape),
                                    B, H, S, D, _PRECISION[precision], num_devices, ctypes.byref(ms)))
     return dq, dk, dv, ms.value
+
+
+def host_release():
+    """Free the device scratch the host-pointer API keeps between calls."""
+    _check(lib().fa2_host_release())

@@ -96,19 +96,27 @@ int fa2_fa1_forward(const float* q, const float* k, const float* v, float* o, fl
 /* ---------------------------------------------------------------------------
  * Host-pointer API: the reference host functions' semantics
  * (kernel_fa2_optimized.cu:350-423, f-attn2-backward.cu:384-485): host buffers
- * in and out, device alloc + H2D + timed kernels + D2H + free, synchronous.
- * *kernel_ms (may be NULL) receives the hipEvent-timed kernel milliseconds
- * (what TimerManager accumulates; copies excluded).
+ * in and out, H2D + timed kernels + D2H, synchronous (returns with the outputs
+ * in the caller's buffers).  *kernel_ms (may be NULL) receives the hipEvent-timed
+ * kernel milliseconds (what TimerManager accumulates; copies excluded).
  *
  * num_devices > 1 shards the B*H heads contiguously over devices 0..n-1, one
  * host thread per device, each copying only its slice (no
  * collective).  *kernel_ms is then the max over devices.
+ *
+ * Unlike the reference (hipMalloc / hipFree of every tensor per call), the device
+ * scratch is kept between calls (one grow-only block per device); each shard runs
+ * as a pipeline over head chunks, the H2D of the next chunk and the D2H of the
+ * previous one overlapping the current chunk's kernels.  fa2_host_release frees
+ * the scratch (the next call allocates it again).
  * ------------------------------------------------------------------------- */
 int fa2_forward_host(const float* q, const float* k, const float* v, float* o, float* lse, int batch, int heads,
                      int seq, int head_dim, int precision, int num_devices, float* kernel_ms);
 int fa2_backward_host(const float* q, const float* k, const float* v, const float* o, const float* dout,
                       const float* lse, float* dq, float* dk, float* dv, int batch, int heads, int seq, int head_dim,
                       int precision, int num_devices, float* kernel_ms);
+
+int fa2_host_release(void);
 
 /* Shard helper shared by the C++ and Python drivers: heads [*first, *first+*count)
  * of `total_heads` belong to shard `index` of `shards` (contiguous, balanced). */
@@ -120,7 +128,8 @@ int fa2_shard_range(int total_heads, int shards, int index, int* first, int* cou
  * FWD_WAVES, FWD_KS, DKDV_WAVES, DKDV_QS, DQ_WAVES, DQ_KS, BWD_FUSED,
  * BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW (see the launchers in kernels/), and
  * the test-only HOST_SHARDS_ON_DEVICE0 = 1 (fa2_*_host run every shard on device 0,
- * so an N-way split's head offsets are testable on one GPU).  Any other name:
+ * so an N-way split's head offsets are testable on one GPU) and HOST_CHUNKS (head
+ * chunks of the fa2_*_host pipeline; 0 = auto).  Any other name:
  * FA2_E_INVALID.  Process-wide.
  * fa2_tune_get: 1 and *value when `knob` is overridden, 0 when it is not,
  * FA2_E_INVALID for an unknown name. */

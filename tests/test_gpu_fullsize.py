@@ -216,16 +216,19 @@ def test_c5_host_api_8way_split(c5_data):
         assert np.array_equal(heads(a, sl), b)
 
 
-def test_host_api_shards_on_one_device_small():
+@pytest.mark.parametrize("chunks", [0, 2, 3])
+def test_host_api_shards_on_one_device_small(chunks):
     """Uneven 3-way split (7 heads: 3 + 2 + 2) of a small problem through the host API on
     device 0, against the oracle: the shard offsets of O, LSE (a [heads][S] vector) and
-    the gradients."""
+    the gradients; with each shard's H2D / kernels / D2H pipeline over 1 (auto), 2 or 3
+    head chunks (HOST_CHUNKS; 3 chunks of a 2-head shard fall back to 2)."""
     B, H, S, D = 1, 7, 300, 64
     q, k, v = fo.cli_inputs(B, H, S, D, seed=5)
     do = np.random.RandomState(6).randn(B, H, S, D).astype(np.float32)
     eo, el = c_oracle.forward(q, k, v, NT)
     edq, edk, edv = c_oracle.backward(q, k, v, eo, do, el, NT)
     fa2amd.tune_set("HOST_SHARDS_ON_DEVICE0", 1)
+    fa2amd.tune_set("HOST_CHUNKS", chunks)
     try:
         for precision, tol in (("fp32", 1e-3), ("fp16", 1e-2)):
             o, lse, _ = fa2amd.forward_host(q, k, v, precision, num_devices=3)

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Wall time of the host-pointer API (fa2_forward_host, fa2_backward_host) per call at
+C3 and C5 on this box's GPUs, for several head-chunk counts (HOST_CHUNKS); with
+--shards-on-device0 N also C5 split N ways with every shard on device 0."""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "cuda-flash-attention_amd"))
+
+
+def timed(fa2amd, shape, ndev, runs):
+    B, H, S, D = shape
+    g = np.random.default_rng(1)
+    q, k, v = (g.random(shape, dtype=np.float32) for _ in range(3))
+    do = np.ones_like(q)
+    o, lse = np.empty_like(q), np.empty((B, H, S), np.float32)
+    dq, dk, dv = np.empty_like(q), np.empty_like(q), np.empty_like(q)
+    tf, tb = [], []
+    for i in range(runs + 1):
+        t0 = time.perf_counter()
+        fa2amd.forward_host(q, k, v, "fp16", num_devices=ndev, out=o, lse=lse)
+        t1 = time.perf_counter()
+        fa2amd.backward_host(q, k, v, o, do, lse, "fp16", num_devices=ndev, dq=dq, dk=dk, dv=dv)
+        t2 = time.perf_counter()
+        if i:
+            tf.append(t1 - t0)
+            tb.append(t2 - t1)
+    fb = 4 * B * H * S * (4 * D + 1)
+    bb = 4 * B * H * S * (8 * D + 1)
+    f, b = statistics.median(tf), statistics.median(tb)
+    return {"fwd_ms": round(f * 1e3, 2), "fwd_gbps": round(fb / f / 1e9, 1), "bwd_ms": round(b * 1e3, 2),
+            "bwd_gbps": round(bb / b / 1e9, 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shards-on-device0", type=int, default=0)
+    args = ap.parse_args()
+    import fa2amd
+
+    out = {}
+    for ch in (1, 2, 4, 0):
+        fa2amd.tune_set("HOST_CHUNKS", ch)
+        out[f"c3_chunks{ch or 'auto'}"] = timed(fa2amd, (4, 16, 2048, 64), 1, 4)
+    fa2amd.tune_set(None)
+    out["c5_auto"] = timed(fa2amd, (64, 16, 2048, 64), 1, 2)
+    if args.shards_on_device0:
+        fa2amd.tune_set("HOST_SHARDS_ON_DEVICE0", 1)
+        out[f"c5_{args.shards_on_device0}shards_dev0"] = timed(fa2amd, (64, 16, 2048, 64), args.shards_on_device0, 2)
+    fa2amd.tune_set(None)
+    fa2amd.host_release()
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
