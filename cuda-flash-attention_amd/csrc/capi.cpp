@@ -65,7 +65,7 @@ std::atomic<int> g_tune_n{0};
 // so a misspelt knob cannot silently leave an A/B on the default plan)
 const char* const kKnobs[] = {"FWD_WAVES", "FWD_KS",    "DKDV_WAVES", "DKDV_QS", "DQ_WAVES",        "DQ_KS",
                               "BWD_FUSED", "BWD_FUSED_DELTA", "BWD_FQS", "BWD_FKS", "BWD_FNW",
-                              "BWD_SP", "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS"};
+                              "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS"};
 bool known_knob(const char* k) {
     for (const char* n : kKnobs)
         if (!strcmp(n, k)) return true;
@@ -188,32 +188,6 @@ int fa2_backward(const float* q, const float* k, const float* v, const float* o,
         : precision == FA2_BF16 ? fa2::launch_backward_bf16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st)
                                 : fa2::launch_backward_f32(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st);
     return hip_status(e, "fa2_backward launch");
-}
-
-int fa2_backward_workspace_size(int B, int H, int S, int D, int precision, unsigned long long* bytes) {
-    int rc;
-    if ((rc = check_shape(B, H, S, D)) || (rc = check_precision(precision))) return rc;
-    if (!bytes) return fail(FA2_E_INVALID, "null bytes pointer");
-    *bytes = precision == FA2_FP32 ? 0ull : (unsigned long long)fa2::bwd_sp_workspace_bytes(D, B * H, S);
-    return FA2_OK;
-}
-
-int fa2_backward_ws(const float* q, const float* k, const float* v, const float* o, const float* dout,
-                    const float* lse, float* delta, float* dq, float* dk, float* dv, int B, int H, int S, int D,
-                    int precision, void* workspace, unsigned long long workspace_bytes, void* stream) {
-    int rc;
-    if ((rc = check_shape(B, H, S, D)) || (rc = check_precision(precision)) ||
-        (rc = check_ptrs({q, k, v, o, dout, lse, delta, dq, dk, dv})))
-        return rc;
-    const hipStream_t st = static_cast<hipStream_t>(stream);
-    const size_t wb = (size_t)workspace_bytes;
-    const hipError_t e =
-        precision == FA2_FP16
-            ? fa2::launch_backward_ws_f16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, workspace, wb, st)
-        : precision == FA2_BF16
-            ? fa2::launch_backward_ws_bf16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, workspace, wb, st)
-            : fa2::launch_backward_f32(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st);
-    return hip_status(e, "fa2_backward_ws launch");
 }
 
 int fa2_backward_dkdv(const float* q, const float* k, const float* v, const float* dout, const float* lse,

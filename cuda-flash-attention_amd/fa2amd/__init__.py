@@ -32,14 +32,14 @@ SUPPORTED_HEAD_DIMS = (32, 64, 128)
 
 # exported symbols of include/fa2_amd.h (checked by tests/test_capi_symbols.py)
 C_SYMBOLS = (
-    "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_ws", "fa2_backward_workspace_size", "fa2_backward_dkdv", "fa2_backward_dq", "fa2_backward_dq_delta",
+    "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv", "fa2_backward_dq", "fa2_backward_dq_delta",
     "fa2_naive_forward", "fa2_fa1_forward",
     "fa2_forward_host", "fa2_backward_host", "fa2_host_release", "fa2_shard_range", "fa2_tune_set", "fa2_tune_get", "fa2_last_error",
     "fa2_version", "fa2_build_id", "fa2_device_count",
 )
 # launch-plan overrides fa2_tune_set accepts (include/fa2_amd.h)
 KNOBS = ("FWD_WAVES", "FWD_KS", "DKDV_WAVES", "DKDV_QS", "DQ_WAVES", "DQ_KS", "BWD_FUSED", "BWD_FUSED_DELTA",
-         "BWD_FQS", "BWD_FKS", "BWD_FNW", "BWD_SP", "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS")
+         "BWD_FQS", "BWD_FKS", "BWD_FNW", "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS")
 
 
 class FA2Error(RuntimeError):
@@ -88,8 +88,6 @@ def _load(path):
         "fa2_forward": [P] * 5 + [I] * 5 + [V],
         "fa2_delta": [P] * 3 + [I] * 4 + [V],
         "fa2_backward": [P] * 10 + [I] * 5 + [V],
-        "fa2_backward_ws": [P] * 10 + [I] * 5 + [V, ctypes.c_ulonglong, V],
-        "fa2_backward_workspace_size": [I] * 5 + [ctypes.POINTER(ctypes.c_ulonglong)],
         "fa2_backward_dkdv": [P] * 8 + [I] * 4 + [V],
         "fa2_backward_dq": [P] * 7 + [I] * 4 + [V],
         "fa2_backward_dq_delta": [P] * 8 + [I] * 4 + [V],
@@ -268,12 +266,8 @@ def delta(dout, o, out=None, stream=None):
     return out
 
 
-def backward(q, k, v, o, dout, lse, precision="fp16", dq=None, dk=None, dv=None, delta_buf=None, stream=None,
-             workspace=None):
-    """dQ, dK, dV = FA2 backward (Δ computed internally into ``delta_buf``).  The
-    single-pass plan's workspace (fa2_backward_ws) comes from torch's allocator unless
-    ``workspace`` (a uint8 device tensor of at least backward_workspace_size bytes) is
-    given."""
+def backward(q, k, v, o, dout, lse, precision="fp16", dq=None, dk=None, dv=None, delta_buf=None, stream=None):
+    """dQ, dK, dV = FA2 backward (Δ computed internally into ``delta_buf``)."""
     import torch
 
     B, H, S, D = _shape(q)
@@ -283,29 +277,8 @@ def backward(q, k, v, o, dout, lse, precision="fp16", dq=None, dk=None, dv=None,
     delta_buf = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if delta_buf is None else delta_buf
     ptrs = _ptrs(((q, "q", 4), (k, "k", 4), (v, "v", 4), (o, "o", 4), (dout, "dout", 4), (lse, "lse", 3),
                   (delta_buf, "delta", 3), (dq, "dq", 4), (dk, "dk", 4), (dv, "dv", 4)), B, H, S, D, q.device)
-    L = lib()
-    prec = _PRECISION[precision]
-    nb = ctypes.c_ulonglong(0)
-    if hasattr(L, "fa2_backward_ws"):
-        _check(L.fa2_backward_workspace_size(B, H, S, D, prec, ctypes.byref(nb)))
-    if nb.value:
-        # the single-pass plan's workspace, from torch's stream-ordered caching allocator
-        ws = workspace if workspace is not None else torch.empty(nb.value, dtype=torch.uint8, device=q.device)
-        if ws.numel() < nb.value or ws.device != q.device:
-            raise ValueError("workspace too small or on another device")
-        _check(L.fa2_backward_ws(*ptrs, B, H, S, D, prec, ctypes.c_void_p(ws.data_ptr()), nb,
-                                 _stream(stream, q.device)))
-    else:
-        _check(L.fa2_backward(*ptrs, B, H, S, D, prec, _stream(stream, q.device)))
+    _check(lib().fa2_backward(*ptrs, B, H, S, D, _PRECISION[precision], _stream(stream, q.device)))
     return dq, dk, dv
-
-
-def backward_workspace_size(B, H, S, D, precision="fp16") -> int:
-    """Bytes of workspace fa2_backward_ws wants for this shape (0: its plan does not
-    apply or is not chosen; fa2_backward's plans run then)."""
-    nb = ctypes.c_ulonglong(0)
-    _check(lib().fa2_backward_workspace_size(B, H, S, D, _PRECISION[precision], ctypes.byref(nb)))
-    return int(nb.value)
 
 
 def backward_dkdv(q, k, v, dout, lse, delta_buf, dk, dv, stream=None):

@@ -1196,605 +1196,6 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
                                            O);
 }
 
-// ===========================================================================
-// Single-pass backward (D <= 64): dK, dV AND dQ from one launch, nothing recomputed
-// ===========================================================================
-// The dK/dV kernel's workgroup (8 waves x 32 keys of one head, the head's 64-query
-// steps streamed through LDS) also produces dQ.  Each step's dS -- already packed to
-// fp16 as the dKᵀ operand -- goes to an LDS image [256 keys][64 queries]; during the
-// next step the workgroup computes dQᵀ_part = Kᵀ·dSᵀ for those 64 queries over its
-// 256 keys on 16x16x32 (Kᵀ by transposed reads of a K image kept in LDS for the whole
-// launch).  5 GEMMs of 2·S²D, the algorithm's count; the two-kernel plan executes 7
-// (S and dP twice).  Reference: f-attn2-backward.cu:119-338, whose dQ leaves by
-// atomicAdd (:269-301).
-//
-// Summing dQ over the head's NKB = ceil(S / 256) key blocks -- no float atomics (gfx950
-// runs those memory-side at ≈1.3 TB/s: 256 MiB of adds at C3, a 200 us floor) and no
-// wait of any kind:
-//   * every wave stores its part of a step (16 queries x D/2 columns, 2 KB at D = 64)
-//     write-through (sc1) into a workspace slot [head][step][key block][wave];
-//   * once those stores have completed (the wait at the next step's end, which costs
-//     nothing: the step's staging loads were waited for just before) it adds one to
-//     the counter [head][step][wave] (agent-scope atomic, result unused);
-//   * the step's owner, key block t mod NKB, reads the counter SP_LAG steps later (and
-//     again every step until it is complete: a head's workgroups drift a few steps
-//     apart); once all NKB parts are in, it queues the step (a per-wave ring in LDS) and reduces it
-//     one chunk of 4 parts per step -- each chunk loaded (sc1) at one step's end and
-//     summed at the next, in key-block order -- stores dQ and adds one more (NKB + 1
-//     marks the step reduced).  Ownership spreads the reductions evenly (r03: handing
-//     each step to the LAST arriving workgroup instead made the slowest workgroup of a
-//     head the reducer of every step, 2.1x slower at C3, 5x at S = 4096);
-//   * a step whose parts were not all in when its owner looked (skew between a head's
-//     workgroups, and the last SP_LAG steps) is left to the head's last workgroup to
-//     finish: after every wave's stores have drained, one lane per workgroup adds to a
-//     per-head counter, and the workgroup whose add returns NKB - 1 sweeps every step
-//     not marked reduced.
-// The order of every sum is fixed, so dQ is bitwise reproducible whoever reduces it;
-// loads see the parts because every part is stored and loaded sc1 and every counter
-// add comes after the storing wave's wait (MI355X_MICROARCH §visibility, table row 1,
-// the wave as the storing unit; the per-head count with the workgroup as the unit).
-// Nothing waits on another workgroup, so no residency, dispatch-order or placement
-// assumption is made.
-// The counters are zeroed by the Δ pass launched just before (fa2_sp_prep_kernel).
-constexpr int SP_KEYS = 256;   // keys per workgroup: 8 waves x 32
-constexpr int SP_QLEN = 256;   // per-wave ring of pending reductions (query steps): S <= 16384
-constexpr int SP_CHUNK = 4;    // parts per reduction chunk
-#ifndef SP_LAG_TICKS
-#define SP_LAG_TICKS 4
-#endif
-constexpr int SP_LAG = SP_LAG_TICKS;  // ticks between a query step and its owner's first counter check
-// Timing-only ablations (variant builds, -DSP_ABL=bits; wrong dQ): 1 no hand-off, 2 no dQ
-// product and no dS image, 4 no owner reductions, 8 no sweep, 16 no per-step wait,
-// 32 no arrival adds, 64 no part stores, 128 part stores plain (not sc1), 256 one m-block stored.
-#ifndef SP_ABL
-#define SP_ABL 0
-#endif
-
-template <int D>
-struct SpLds {
-    static constexpr int QT = 64, TILE = QT * D;         // halves
-    static constexpr int KI = 4 * TILE;                   // after the [2][Q | dO] tiles: the K image [256][D]
-    static constexpr int DSI = KI + SP_KEYS * D;          // [2] dSᵀ images [256 keys][64 queries]
-    static constexpr int DSIMG = SP_KEYS * QT;
-    static constexpr int HALVES = DSI + 2 * DSIMG;
-    static constexpr int ROWS = 2 * HALVES;               // bytes: [2][-lse2 | -delta][64] fp32
-    static constexpr int QUEUE = ROWS + 2 * 2 * QT * 4;   // [8 waves][SP_QLEN] u16
-    static constexpr int BYTES = QUEUE + 8 * SP_QLEN * 2;
-    static_assert(8 * 32 * 36 * 4 <= 2 * 2 * DSIMG, "the epilogue stage fits over the dS images");
-};
-
-// Per-lane offsets of the single-pass kernel's own accesses.  Wave w owns the dQ tiles
-// of queries 16 (w & 3) .. +15 of a step and d-blocks (w >> 2) D/32 .. +D/32-1 (of 16).
-template <int D>
-struct SpOffsets {
-    int dsw[2][2];      // dS write, query block qb, k-slots 4h..4h+3: row key (l & 15), col qb*32 + 16h + 4g
-    int ka[D / 32][2];  // transposed K-image reads (rows 4g + q / 16 + 4g + q) of the wave's d-blocks
-    int db[2];          // transposed dSᵀ-image reads of the wave's 16 queries
-    int voff[D / 32];   // byte offset of the lane's 4 dQ values inside a 64-query step
-    int qrow;           // the lane's query row inside a step
-    __device__ __forceinline__ void init(int lane, int wave) {
-        const int i = lane & 15, g = lane >> 4, q = i >> 2, p4 = i & 3;
-        const int qblk = wave & 3, md0 = (wave >> 2) * (D / 32);
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) dsw[qb][h] = tile_off<64>(wave * 32 + i, qb * 32 + 16 * h + 4 * g);
-#pragma unroll
-        for (int m = 0; m < D / 32; ++m) {
-            ka[m][0] = tile_off<D>(4 * g + q, 16 * (md0 + m) + 4 * p4);
-            ka[m][1] = tile_off<D>(16 + 4 * g + q, 16 * (md0 + m) + 4 * p4);
-            voff[m] = ((16 * qblk + i) * D + 16 * (md0 + m) + 4 * g) * 4;
-        }
-        db[0] = tile_off<64>(4 * g + q, 16 * qblk + 4 * p4);
-        db[1] = tile_off<64>(16 + 4 * g + q, 16 * qblk + 4 * p4);
-        qrow = 16 * qblk + i;
-    }
-};
-
-// One 64-query step for the wave's 32 keys: dkdv_step16's four products, plus the
-// step's dS (the dKᵀ B operand) written to the dSᵀ image.  Keys >= S need no mask:
-// their K-image rows are zero, so they add nothing to dQ, and their dK / dV rows are
-// never stored.
-template <int D, typename Mid>
-__device__ __forceinline__ void sp_step(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
-                                        const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
-                                        const SpOffsets<D>& oo, _Float16* dsimg, int g, Mid&& mid) {
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-        if (qb == 1) mid();
-        f32x4 sa[2][2], da[2][2];  // [mb][nb]
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            const f32x4 lv = *reinterpret_cast<const f32x4*>(nlse2 + qb * 32 + 16 * mb + 4 * g);
-            const f32x4 dv = *reinterpret_cast<const f32x4*>(ndel + qb * 32 + 16 * mb + 4 * g);
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                sa[mb][nb] = lv;
-                da[mb][nb] = dv;
-            }
-        }
-#pragma unroll
-        for (int ks = 0; ks < D / 32; ++ks)
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb) {
-                const f16x8 qa = fo.rowop(Qs, qb * 32 + 16 * mb, ks), doa = fo.rowop(dOs, qb * 32 + 16 * mb, ks);
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    sa[mb][nb] = mfma16(qa, st.kf[nb][ks], sa[mb][nb]);
-                    da[mb][nb] = mfma16(doa, st.vf[nb][ks], da[mb][nb]);
-                }
-            }
-        f16x8 pf[2], dsf[2];  // [nb], k-slot j <-> query 16 (j >> 2) + 4g + (j & 3)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-                const float p0 = fast_exp2(sa[j >> 2][nb][j & 3]), p1 = fast_exp2(sa[j >> 2][nb][(j & 3) + 1]);
-                pf[nb][j] = to_tile(p0);
-                pf[nb][j + 1] = to_tile(p1);
-                const tile2 d2 = ds_pair(p0, p1, da[j >> 2][nb][j & 3], da[j >> 2][nb][(j & 3) + 1], pf[nb][j],
-                                         pf[nb][j + 1]);
-                dsf[nb][j] = d2[0];
-                dsf[nb][j + 1] = d2[1];
-            }
-        // dS into the dSᵀ image: k-slots 0..3 are queries qb*32 + 4g + 0..3, 4..7 are
-        // qb*32 + 16 + 4g + 0..3, of key row 16 nb + (l & 15)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            if (SP_ABL & 2) break;
-            const i16x8 v = __builtin_bit_cast(i16x8, dsf[nb]);
-            *reinterpret_cast<i16x4*>(dsimg + oo.dsw[qb][0] + nb * 16 * 64) = __builtin_shufflevector(v, v, 0, 1, 2, 3);
-            *reinterpret_cast<i16x4*>(dsimg + oo.dsw[qb][1] + nb * 16 * 64) = __builtin_shufflevector(v, v, 4, 5, 6, 7);
-        }
-#pragma unroll
-        for (int md = 0; md < D / 16; ++md) {
-            const f16x8 a_do = fo.trop(dOs, qb * 32, md), a_q = fo.trop(Qs, qb * 32, md);
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                st.dva[md][nb] = mfma16(a_do, pf[nb], st.dva[md][nb]);
-                st.dka[md][nb] = mfma16(a_q, dsf[nb], st.dka[md][nb]);
-            }
-        }
-    }
-}
-
-// The wave's dQ part of one step: dQᵀ rows d of its D/32 16-blocks, columns its 16
-// queries, summed over the workgroup's 256 keys.  A = Kᵀ (transposed reads of the K
-// image), B = dSᵀ (transposed reads of the step's image): both take a k-step's 32 keys
-// in the same packed order 16 (j >> 2) + 4g + (j & 3), so the sum is exact.  The K
-// image holds K·log2e/√D; the final sum is scaled by ln 2 to dS·K/√D.
-template <int D>
-__device__ __forceinline__ void sp_dq(f32x4 (&acc)[D / 32], const _Float16* kimg, const _Float16* dsimg,
-                                      const SpOffsets<D>& oo) {
-#pragma unroll
-    for (int m = 0; m < D / 32; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < SP_KEYS / 32; ++kk) {
-        const f16x8 b = cat4(lds_tr4(dsimg + oo.db[0] + kk * 32 * 64), lds_tr4(dsimg + oo.db[1] + kk * 32 * 64));
-#pragma unroll
-        for (int m = 0; m < D / 32; ++m)
-            acc[m] = mfma16(cat4(lds_tr4(kimg + oo.ka[m][0] + kk * 32 * D), lds_tr4(kimg + oo.ka[m][1] + kk * 32 * D)),
-                            b, acc[m]);
-    }
-}
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) unsigned gu32;
-
-// buffer descriptor over `bytes` bytes at p (wave-uniform values only)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(const void* p, unsigned bytes) {
-    const unsigned long long a = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0,
-                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-constexpr int SP_SC1 = 16;  // cache-policy operand of the buffer ops: sc1 (write-through / L2-served)
-
-// Workspace of the single-pass backward: the parts [bh][step][key block][wave][m][lane]
-// (f32x4, D/32 m-blocks), then the counters [bh][step][wave] (u32).
-struct SpWs {
-    // per head: [step][m][key block][wave] slots of 1 KB (64 lanes x f32x4), steps
-    // 0..nqs-1 and one junk step (stores with nothing to store go there)
-    static __host__ __device__ long head_part_bytes(int D, int S) {
-        const long nqs = (S + 63) / 64, nkb = (S + SP_KEYS - 1) / SP_KEYS;
-        return (nqs + 1) * nkb * 8 * (D / 32) * 1024;
-    }
-    static __host__ __device__ int part_soff(int t, int m, int kb, int nkb, int wave, int MD) {
-        return (((t * MD + m) * nkb + kb) * 8 + wave) * 1024;
-    }
-    // per head: [step][wave], then 8 words whose first counts the head's finished workgroups
-    static __host__ __device__ long counters(int S) { return (long)((S + 63) / 64) * 8 + 8; }
-    static __host__ __device__ long bytes(int D, int bh, int S) {
-        return (long)bh * (head_part_bytes(D, S) + 4 * counters(S));
-    }
-};
-
-template <int N>
-struct SpPar {
-    static constexpr int value = N;
-};
-
-// ONE: the head has one key block (S <= 256): its parts are dQ itself, no hand-off (a
-// template parameter, not a runtime branch: see emit_part)
-template <int D, bool ONE>
-__global__ void __launch_bounds__(512)
-fa2_bwd_sp_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                      const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-                      float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV, int S,
-                      char* __restrict__ ws) {
-    static_assert(D == 32 || D == 64, "single-pass backward: D <= 64");
-    using L = SpLds<D>;
-    constexpr int QT = L::QT, TILE = L::TILE, NT = 512, MD = D / 32;
-    __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
-    _Float16* const smem = reinterpret_cast<_Float16*>(lds);
-    _Float16* const kimg = smem + L::KI;
-    _Float16* const dsimg = smem + L::DSI;
-    float(*rows)[2][QT] = reinterpret_cast<float(*)[2][QT]>(lds + L::ROWS);
-    float(*ostage)[32][36] = reinterpret_cast<float(*)[32][36]>(lds + 2 * L::DSI);  // epilogue: over the dS images
-
-    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    unsigned short* const ring = reinterpret_cast<unsigned short*>(lds + L::QUEUE) + wave * SP_QLEN;
-    const int nkb = ONE ? 1 : (S + SP_KEYS - 1) / SP_KEYS, nqs = (S + QT - 1) / QT;
-    const int nbh = gridDim.x / nkb;
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = bid / nkb, kblk = bid - bh * nkb;
-    const long base = (long)bh * S * D, rbase = (long)bh * S;
-    const int key0 = kblk * SP_KEYS, wkey0 = key0 + wave * 32;
-    const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
-
-    const long hpart = SpWs::head_part_bytes(D, S);
-    const __amdgpu_buffer_rsrc_t rs_part = ws_rsrc(ws + (long)bh * hpart, (unsigned)hpart);
-    unsigned* const cnt = reinterpret_cast<unsigned*>(ws + (long)nbh * hpart) + (long)bh * SpWs::counters(S) + wave;
-    const __amdgpu_buffer_rsrc_t rs_lse = head_rsrc(LSE + rbase, S, 1);
-    const __amdgpu_buffer_rsrc_t rs_del = head_rsrc(Delta + rbase, S, 1);
-    float* const dqh = dQ + base;
-
-    FragOffsets16<D> fo;
-    fo.init(lane);
-    SpOffsets<D> oo;
-    oo.init(lane, wave);
-    DkdvState16<D> st;
-    TileStager<D, QT, NT> qs, dos;
-    float rowraw = 0.f;
-    int rowq = 0;
-    auto load_step = [&](int q0) {
-        qs.load(q0);
-        dos.load(q0);
-        if (wave < 2) {
-            rowq = q0 + lane;
-            rowraw = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wave == 0 ? rs_lse : rs_del,
-                                                                                     lane * 4, q0 * 4, 0));
-        }
-    };
-    auto store_step = [&](int b) {
-        qs.store(smem + 2 * b * TILE, 1.f, tid);
-        dos.store(smem + (2 * b + 1) * TILE, 1.f, tid);
-        // stored negated: the initial accumulators of S and dP
-        if (wave == 0) rows[b][0][lane] = rowq < S ? -rowraw * FA2B_LOG2E : -__builtin_inff();
-        else if (wave == 1) rows[b][1][lane] = -rowraw;
-    };
-
-    // prologue: K (kept as the K image) and V (through dS image 1, first written in
-    // step 1) of the workgroup's 256 keys, and the first step's Q, dO and row constants
-    {
-        TileStager<D, SP_KEYS, NT> kst, vst;
-        kst.init(K + base, S, tid);
-        vst.init(V + base, S, tid);
-        kst.load(key0);
-        vst.load(key0);
-        qs.init(Q + base, S, tid);
-        dos.init(dO + base, S, tid);
-        load_step(0);
-        kst.store(kimg, kscale, tid);
-        vst.store(dsimg + L::DSIMG, 1.f, tid);
-        store_step(0);
-        __syncthreads();
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int ks = 0; ks < D / 32; ++ks) {
-                st.kf[nb][ks] = fo.rowop(kimg, wave * 32 + 16 * nb, ks);
-                st.vf[nb][ks] = fo.rowop(dsimg + L::DSIMG, wave * 32 + 16 * nb, ks);
-            }
-#pragma unroll
-        for (int md = 0; md < D / 16; ++md)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                st.dka[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-                st.dva[md][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-    }
-
-    // ---- dQ hand-off.  Every state variable is wave-uniform and is re-read through
-    // readfirstlane where it is used: loop-carried, the compiler keeps such values in
-    // VGPRs, turns each branch on them into an exec mask (with a full vmcnt(0) drain in
-    // front of the masked block) and each buffer offset derived from them into a
-    // waterfall loop (r03 ISA audit: 2 x 4 of those per step).
-#define SPU(x) __builtin_amdgcn_readfirstlane(x)
-    const long cnt_bytes = SpWs::counters(S) * 4;
-    const __amdgpu_buffer_rsrc_t rs_cnt = ws_rsrc(ws + (long)nbh * hpart + (long)bh * cnt_bytes, (unsigned)cnt_bytes);
-    // (No out-of-range tricks for the stores and adds below: r03 measured buffer stores
-    // and atomics at an offset past num_records taking effect -- wrong, unrepeatable dQ --
-    // so a lane or step with nothing to store writes the wave's junk slot instead.)
-    char* const junk = ws + (long)bh * hpart + (long)SpWs::part_soff(nqs, 0, kblk, nkb, wave, MD) + lane * 16;
-    f32x4 part[MD];              // this wave's dQ part of the step before
-    int chk_next = kblk;         // the owner's oldest step not yet seen complete
-    int chk_t = -1;              // step of the counter check in flight
-    unsigned chk_v = 0;          // its value
-    int qh = 0, qt = 0;          // ring head / tail
-    int red_t = -1, red_m = 0, red_kb0 = 0;  // the reduction being issued and its next chunk
-    int ch_t = -1, ch_m = 0, ch_kb0 = 0;     // the chunk in flight (ch_t < 0: none)
-    f32x4 ch[SP_CHUNK];
-    f32x4 rsum = {0.f, 0.f, 0.f, 0.f};
-    auto part_soff = [&](int t, int kb, int m) { return SpWs::part_soff(t, m, kb, nkb, wave, MD); };
-    // dQ rows of step t, m-block m (a lane whose row is >= S stores to the junk slot)
-    auto final_store = [&](int t, int m, f32x4 v) {
-        const int q = t * QT + oo.qrow;
-        char* const dst = q < S ? reinterpret_cast<char*>(dqh) + (long)t * QT * D * 4 + (m == 0 ? oo.voff[0] : oo.voff[MD - 1])
-                                : junk;
-        *reinterpret_cast<f32x4*>(dst) = v * 0.6931471805599453f;
-    };
-    // counter [t][wave] += v from lane 0 alone, result unused.  Inline asm with EXEC
-    // narrowed to lane 0 inside it: a C++ `if (lane == 0)` is an exec-masked block the
-    // compiler may branch around, after which it can no longer count the VMEM ops in
-    // flight and drains them all (vmcnt(0)) at the next wait (r03 ISA audit).
-    auto cnt_add = [&](int t, int v) {
-        unsigned* const p = cnt + (long)t * 8;
-        unsigned long long sv;
-        asm volatile(
-            "s_mov_b64 %0, exec\n\t"
-            "s_mov_b64 exec, 1\n\t"
-            "global_atomic_add %1, %2, off\n\t"
-            "s_mov_b64 exec, %0"
-            : "=&s"(sv)
-            : "v"(p), "v"(v)
-            : "memory");
-    };
-    // The part of query step t: one sc1 store per m-block into its slot (nkb == 1: into
-    // dQ itself, scaled); t < 0: into the junk slot.  Always the same MD store
-    // instructions, never skipped by a branch: behind a branch, the wait store_step needs
-    // for the staging loads issued just before becomes a full vmcnt(0) that also drains
-    // these stores (r03 ISA audit).
-    auto emit_part = [&](int t) {
-        if (SP_ABL & 64) return;
-        if constexpr (ONE) {
-#pragma unroll
-            for (int m = 0; m < MD; ++m) final_store(t < 0 ? nqs : t, m, part[m]);  // (step nqs: junk)
-        } else {
-#pragma unroll
-            for (int m = 0; m < ((SP_ABL & 256) ? 1 : MD); ++m)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, part[m]), rs_part, lane * 16,
-                                                       part_soff(t < 0 ? nqs : t, kblk, m),
-                                                       (SP_ABL & 128) ? 0 : SP_SC1);
-        }
-    };
-    auto enqueue = [&](int t) {  // every lane writes the same slot (no exec mask)
-        ring[SPU(qt) & (SP_QLEN - 1)] = (unsigned short)t;
-        qt = SPU(qt) + 1;
-    };
-    auto consume_check = [&] {
-        const int ct = SPU(chk_t);
-        if (ct >= 0) {  // the owner's check: every key block's part of ct is in
-            if (SPU((int)chk_v) == nkb) {
-                enqueue(ct);
-                chk_next = SPU(chk_next) + nkb;
-            }
-            chk_t = -1;  // (else checked again at this tick)
-        }
-    };
-    // End-of-step bookkeeping, after store_step (before the step's closing barrier).
-    // The step's part stores went out mid-step, right after the next step's staging
-    // loads, so the wait store_step needed for those loads did not wait for them; the
-    // wait below leaves exactly those MD stores in flight and covers everything older:
-    // the previous step's part stores (whose arrival is counted here) and the check /
-    // chunk loads of the previous tick.
-    auto tick = [&](int s) {
-        if (!(SP_ABL & 16)) {
-            if constexpr (MD == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        }
-        consume_check();
-        const int cht = SPU(ch_t);
-        if (cht >= 0) {
-            const int kb0 = SPU(ch_kb0), m = SPU(ch_m);
-#pragma unroll
-            for (int c = 0; c < SP_CHUNK; ++c)
-                if (kb0 + c < nkb) rsum = kb0 + c == 0 ? ch[c] : rsum + ch[c];
-            if (kb0 + SP_CHUNK >= nkb) {
-                final_store(cht, m, rsum);
-                if (m == MD - 1) cnt_add(cht, 1);  // reduced: the counter reads NKB + 1
-            }
-            ch_t = -1;
-        }
-        if (!ONE) {
-            // arrival: the part of query step s - 2, stored mid-way through the previous
-            // step, is complete
-            if (!(SP_ABL & 32) && s >= 2 && s - 2 < nqs) cnt_add(s - 2, 1);
-            // the owner (key block t mod NKB) checks the counter of its oldest unconfirmed
-            // step t once it is SP_LAG ticks old, and again every tick until it is complete
-            // (a head's workgroups drift a few steps apart)
-            const int t = SPU(chk_next);
-            if (!(SP_ABL & 4) && t < nqs && t + SP_LAG <= s) {
-                chk_v = __builtin_amdgcn_raw_buffer_load_b32(rs_cnt, (t * 8 + wave) * 4, 0, SP_SC1);
-                chk_t = t;
-            }
-        }
-        // the next chunk of the reduction in progress, or of the next queued step
-        int rt = SPU(red_t);
-        if (rt < 0 && SPU(qh) != SPU(qt)) {
-            rt = SPU((int)ring[SPU(qh) & (SP_QLEN - 1)]);
-            qh = SPU(qh) + 1;
-            red_m = 0;
-            red_kb0 = 0;
-        }
-        if (rt >= 0) {
-            const int m = SPU(red_m), kb0 = SPU(red_kb0);
-#pragma unroll
-            for (int c = 0; c < SP_CHUNK; ++c)
-                if (kb0 + c < nkb)
-                    ch[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          rs_part, lane * 16, part_soff(rt, kb0 + c, m), SP_SC1));
-            ch_t = rt;
-            ch_m = m;
-            ch_kb0 = kb0;
-            if (kb0 + SP_CHUNK < nkb) {
-                red_kb0 = kb0 + SP_CHUNK;
-            } else if (m + 1 < MD) {
-                red_m = m + 1;
-                red_kb0 = 0;
-            } else {
-                rt = -1;
-            }
-        }
-        red_t = rt;
-    };
-    // a whole reduction of query step t (this wave's slice) at once: up to 8 parts per
-    // m-block in flight, summed in key-block order, stored, the counter marked
-    auto reduce_now = [&](int t, int mark) {
-        t = SPU(t);
-#pragma unroll
-        for (int m = 0; m < MD; ++m) {
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            for (int kb0 = 0; kb0 < nkb; kb0 += 8) {
-                f32x4 v[8];
-#pragma unroll
-                for (int c = 0; c < 8; ++c)
-                    if (kb0 + c < nkb)
-                        v[c] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                             rs_part, lane * 16, part_soff(t, kb0 + c, m), SP_SC1));
-#pragma unroll
-                for (int c = 0; c < 8; ++c)
-                    if (kb0 + c < nkb) acc = kb0 + c == 0 ? v[c] : acc + v[c];
-            }
-            final_store(t, m, acc);
-        }
-        cnt_add(t, mark);
-    };
-
-#ifdef SP_STAMPS
-    unsigned long long st_wait = 0, st_tick = 0, st_bar = 0, st_step = 0, st_last = __builtin_amdgcn_s_memtime();
-#endif
-    auto step = [&](auto B_, int t) {
-        constexpr int b = decltype(B_)::value;
-        const bool more = t + 1 < nqs;
-        // between the step's two query blocks: the next step's staging loads, then the
-        // previous step's dQ part (from its dS image) and its stores
-        sp_step<D>(st, smem + 2 * b * TILE, smem + (2 * b + 1) * TILE, rows[b][0], rows[b][1], fo, oo,
-                   dsimg + b * L::DSIMG, g, [&] {
-                       if (more) load_step((t + 1) * QT);
-                       // (at t = 0 the product reads V from image 1 and its stores are dropped)
-                       if (!(SP_ABL & 2)) sp_dq<D>(part, kimg, dsimg + (b ^ 1) * L::DSIMG, oo);
-                       if (SP_ABL & 1) {
-                           if (S < 0) final_store(t, 0, part[0]);  // keeps the product alive
-                       } else {
-                           emit_part(t - 1);
-                       }
-                   });
-#ifdef SP_STAMPS
-        const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-#endif
-        if (more) store_step(b ^ 1);
-#ifdef SP_STAMPS
-        const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-#endif
-        if (!(SP_ABL & 1)) tick(t);
-#ifdef SP_STAMPS
-        const unsigned long long c2 = __builtin_amdgcn_s_memtime();
-#endif
-        __syncthreads();
-#ifdef SP_STAMPS
-        const unsigned long long c3 = __builtin_amdgcn_s_memtime();
-        st_wait += c1 - c0;
-        st_tick += c2 - c1;
-        st_bar += c3 - c2;
-        st_step += c3 - st_last;
-        st_last = c3;
-#endif
-    };
-    for (int t = 0; t < nqs; t += 2) {
-        step(SpPar<0>{}, t);
-        if (t + 1 < nqs) step(SpPar<1>{}, t + 1);
-    }
-#ifdef SP_STAMPS
-    if (lane == 0) {  // timing build: per wave cycles [store_step wait, tick, barrier, loop] -> its junk slot
-        unsigned long long* js = reinterpret_cast<unsigned long long*>(ws + (long)bh * hpart + SpWs::part_soff(nqs, 0, kblk, nkb, wave, MD));
-        js[0] = st_wait; js[1] = st_tick; js[2] = st_bar; js[3] = st_step;
-    }
-#endif
-    // tail: the last step's part, dK / dV out, then the remaining hand-offs
-    if ((nqs - 1) & 1) sp_dq<D>(part, kimg, dsimg + L::DSIMG, oo);
-    else sp_dq<D>(part, kimg, dsimg, oo);
-    __syncthreads();  // every wave's dS-image reads are done: the images take the stage
-    {
-        const float dscale = 1.f / __builtin_sqrtf((float)D);
-        store_block_rows16<D>(ostage[wave], st.dka, dscale, dK + base + (long)wkey0 * D, S - wkey0, lane);
-        store_block_rows16<D>(ostage[wave], st.dva, 1.f, dV + base + (long)wkey0 * D, S - wkey0, lane);
-    }
-    if (SP_ABL & 1) return;
-    emit_part(nqs - 1);
-    if (ONE) return;
-    // the last check, then every reduction this wave has taken on (their parts are all
-    // in: the owner's check said so), each issued whole; the one in progress is redone
-    // from its first part (same order, same result)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    consume_check();
-    if (SPU(ch_t) >= 0) reduce_now(ch_t, 1);
-    while (SPU(qh) != SPU(qt)) {
-        const int t = SPU((int)ring[SPU(qh) & (SP_QLEN - 1)]);
-        qh = SPU(qh) + 1;
-        reduce_now(t, 1);
-    }
-    // The head's last workgroup to get here reduces every step no owner has: each wave
-    // drains its stores, the workgroup meets, one lane counts it in (MI355X_MICROARCH
-    // §visibility, table row 1: an agent-scope add after every storing wave's wait,
-    // behind a workgroup barrier; the last adder's waves load after the barrier below).
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* const flag = reinterpret_cast<int*>(lds + L::QUEUE);  // the rings are no longer in use
-    if (tid == 0) {
-        const unsigned old = __hip_atomic_fetch_add((gu32*)(cnt - wave + SpWs::counters(S) - 8), 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        flag[0] = old == (unsigned)(nkb - 1);
-    }
-    __syncthreads();
-    if (!flag[0] || (SP_ABL & 8)) return;
-    // sweep: this wave's slice of every step whose counter is not NKB + 1 (lane l reads
-    // the counter of step t0 + l)
-    for (int t0 = 0; t0 < nqs; t0 += 64) {
-        const int t = t0 + lane;
-        const unsigned c = t < nqs ? __builtin_amdgcn_raw_buffer_load_b32(rs_cnt, (t * 8 + wave) * 4, 0, SP_SC1)
-                                   : (unsigned)(nkb + 1);
-        unsigned long long todo = __ballot(c <= (unsigned)nkb);
-        while (todo) {
-            const int l = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            reduce_now(t0 + l, 0x10000);  // (marked apart from the owners' 1: tools/sp_probe.py)
-        }
-    }
-#undef SPU
-}
-
-// Δ = rowsum(dO ∘ O) (as fa2_delta_kernel) and the single-pass counters zeroed, one pass
-template <int D>
-__global__ void __launch_bounds__(256) fa2_sp_prep_kernel(const float* __restrict__ dO, const float* __restrict__ O,
-                                                          float* __restrict__ Dvec, long rows,
-                                                          unsigned* __restrict__ cnt, long ncnt) {
-    constexpr int LPR = D / 4;  // lanes per row
-    const long stride = (long)gridDim.x * (256 / LPR);
-    const int sub = threadIdx.x % LPR;
-    for (long row = (long)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; row < rows; row += stride) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(dO + row * D + 4 * sub);
-        const f32x4 b = *reinterpret_cast<const f32x4*>(O + row * D + 4 * sub);
-        float acc = a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
-#pragma unroll
-        for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-        if (sub == 0) Dvec[row] = acc;
-    }
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < ncnt; i += (long)gridDim.x * 256) cnt[i] = 0u;
-}
-
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
 // block 256, test_flash_attention2.py:499-535 / f-attn2-backward_f16.cu:445),
 // fp16 tiles on MFMA.  A workgroup owns 32 keys (B operands K*log2e/sqrt(D) and
@@ -2188,55 +1589,6 @@ hipError_t launch_bwd_fused_delta(int D, const float* q, const float* k, const f
     }
 }
 }  // namespace
-
-#ifndef FA2_TILE_BF16
-// The single-pass plan applies to D <= 64, S <= 16384.  Chosen (override BWD_SP:
-// 1 = wherever it applies, 0 = never) by default on ... (see below).
-size_t bwd_sp_workspace_bytes(int D, int bh, int S) {
-    if ((D != 32 && D != 64) || bh <= 0 || S <= 0 || S > 64 * fa2f16b::SP_QLEN) return 0;
-    int sp = tune_knob("BWD_SP", -1);
-    if (sp < 0) sp = 0;
-    return sp == 1 ? (size_t)fa2f16b::SpWs::bytes(D, bh, S) : 0;
-}
-#endif
-
-namespace {
-template <int D>
-hipError_t sp_launch(const float* q, const float* k, const float* v, const float* o, const float* dout,
-                     const float* lse, float* delta, float* dq, float* dk, float* dv, int bh, int S, void* ws,
-                     hipStream_t stream) {
-    using W = fa2f16b::SpWs;
-    const long grid = (long)bh * ((S + fa2f16b::SP_KEYS - 1) / fa2f16b::SP_KEYS);
-    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    const long rows = (long)bh * S, per_block = 256 / (D / 4);
-    const long pgrid0 = (rows + per_block - 1) / per_block, pgrid = pgrid0 < 8192 ? pgrid0 : 8192;
-    unsigned* cnt = reinterpret_cast<unsigned*>(static_cast<char*>(ws) + (long)bh * W::head_part_bytes(D, S));
-    hipLaunchKernelGGL((fa2f16b::fa2_sp_prep_kernel<D>), dim3((unsigned)pgrid), dim3(256), 0, stream, dout, o, delta,
-                       rows, cnt, (long)bh * W::counters(S));
-    if (S <= fa2f16b::SP_KEYS)
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_sp_f16_kernel<D, true>), dim3((unsigned)grid), dim3(512), 0, stream, q, k,
-                           v, dout, lse, delta, dq, dk, dv, S, static_cast<char*>(ws));
-    else
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_sp_f16_kernel<D, false>), dim3((unsigned)grid), dim3(512), 0, stream, q,
-                           k, v, dout, lse, delta, dq, dk, dv, S, static_cast<char*>(ws));
-    return hipGetLastError();
-}
-}  // namespace
-
-// fa2_backward with a caller workspace (bwd_sp_workspace_bytes): the single-pass plan
-// where it applies (D <= 64, S <= 16384, workspace large enough), else launch_backward.
-// Override BWD_SP (fa2_tune_set): 1 = single-pass wherever it applies, 0 = never.
-hipError_t FA2_TILE_LAUNCH(launch_backward_ws)(int D, const float* q, const float* k, const float* v, const float* o,
-                                               const float* dout, const float* lse, float* delta, float* dq, float* dk,
-                                               float* dv, int bh, int S, void* ws, size_t ws_bytes,
-                                               hipStream_t stream) {
-    const size_t need = bwd_sp_workspace_bytes(D, bh, S);
-    if (need > 0 && ws && ws_bytes >= need) {
-        if (D == 32) return sp_launch<32>(q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, ws, stream);
-        if (D == 64) return sp_launch<64>(q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, ws, stream);
-    }
-    return FA2_TILE_LAUNCH(launch_backward)(D, q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, stream);
-}
 
 // Override BWD_FUSED (fa2_tune_set): 1 = Δ kernel, then dK/dV and dQ in one launch (D <= 64);
 // 0 = Δ fused into the dQ kernel's prologue (which stages dO anyway), then dK/dV,

@@ -101,16 +101,6 @@ hipError_t launch_bwd_fused_f16(int D, const float* q, const float* k, const flo
                                 const float* lse, const float* delta, float* dq, float* dk, float* dv, int bh, int S,
                                 hipStream_t stream);
 
-// Single-pass backward (dK, dV and dQ in one launch, D <= 64, S <= 16384): the
-// workspace it needs (0 where the plan does not apply), and launch_backward with a
-// caller workspace -- the single-pass plan where it applies and is chosen, else
-// launch_backward_f16.  The workspace needs no initialisation (the plan's Δ pass
-// zeroes its counters).
-size_t bwd_sp_workspace_bytes(int D, int bh, int S);
-hipError_t launch_backward_ws_f16(int D, const float* q, const float* k, const float* v, const float* o,
-                                  const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
-                                  int bh, int S, void* ws, size_t ws_bytes, hipStream_t stream);
-
 // bf16-tile twins of the *_f16 launchers above (kernels built from the same source)
 hipError_t launch_forward_bf16(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,
                                int S, hipStream_t stream);
@@ -125,9 +115,6 @@ hipError_t launch_bwd_dq_bf16(int D, const float* q, const float* k, const float
 hipError_t launch_bwd_fused_bf16(int D, const float* q, const float* k, const float* v, const float* dout,
                                  const float* lse, const float* delta, float* dq, float* dk, float* dv, int bh, int S,
                                  hipStream_t stream);
-hipError_t launch_backward_ws_bf16(int D, const float* q, const float* k, const float* v, const float* o,
-                                   const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
-                                   int bh, int S, void* ws, size_t ws_bytes, hipStream_t stream);
 hipError_t launch_bwd_dq_delta_bf16(int D, const float* q, const float* k, const float* v, const float* o,
                                     const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
                                     hipStream_t stream);

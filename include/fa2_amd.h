@@ -64,19 +64,6 @@ int fa2_backward(const float* q, const float* k, const float* v, const float* o,
                  const float* lse, float* delta, float* dq, float* dk, float* dv, int batch, int heads, int seq,
                  int head_dim, int precision, void* stream);
 
-/* Backward with a caller workspace: the single-pass plan (dK, dV and dQ from ONE
- * launch after the Δ pass, nothing recomputed; D <= 64, seq <= 16384) where it
- * applies and the workspace is large enough, else exactly fa2_backward.  The
- * workspace is device memory of at least fa2_backward_workspace_size() bytes, used
- * by this call only (stream-ordered: reuse it on the same stream, or after the call
- * has finished); it needs no initialisation.  Results are bitwise reproducible, as
- * fa2_backward's.  fa2_backward_workspace_size writes 0 where the plan does not
- * apply (then fa2_backward_ws runs fa2_backward's plans). */
-int fa2_backward_workspace_size(int batch, int heads, int seq, int head_dim, int precision, unsigned long long* bytes);
-int fa2_backward_ws(const float* q, const float* k, const float* v, const float* o, const float* dout,
-                    const float* lse, float* delta, float* dq, float* dk, float* dv, int batch, int heads, int seq,
-                    int head_dim, int precision, void* workspace, unsigned long long workspace_bytes, void* stream);
-
 /* The two MFMA kernels of the fp16 backward, separately (profiling/bench hooks;
  * fa2_delta + these two compute what fa2_backward with FA2_FP16 does). */
 int fa2_backward_dkdv(const float* q, const float* k, const float* v, const float* dout, const float* lse,
@@ -139,7 +126,7 @@ int fa2_shard_range(int total_heads, int shards, int index, int* first, int* cou
  * environment).  fa2_tune_set("DKDV_QS", 2) makes the next launches use that plan
  * where the shape allows it; fa2_tune_set(NULL, 0) clears every override.  Knobs:
  * FWD_WAVES, FWD_KS, DKDV_WAVES, DKDV_QS, DQ_WAVES, DQ_KS, BWD_FUSED,
- * BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW, BWD_SP (see the launchers in kernels/), and
+ * BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW (see the launchers in kernels/), and
  * the test-only HOST_SHARDS_ON_DEVICE0 = 1 (fa2_*_host run every shard on device 0,
  * so an N-way split's head offsets are testable on one GPU) and HOST_CHUNKS (head
  * chunks of the fa2_*_host pipeline; 0 = auto).  Any other name:
