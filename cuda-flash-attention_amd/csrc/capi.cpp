@@ -8,7 +8,6 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
-#include <map>
 #include <mutex>
 #include <cstdio>
 #include <string>
@@ -64,7 +63,7 @@ std::atomic<int> g_tune_n{0};
 
 // the launch-plan overrides the launchers read (fa2_tune_set rejects other names,
 // so a misspelt knob cannot silently leave an A/B on the default plan)
-const char* const kKnobs[] = {"FWD_WAVES", "FWD_KS", "FWD_XS", "DKDV_WAVES", "DKDV_QS", "DQ_WAVES",        "DQ_KS",
+const char* const kKnobs[] = {"FWD_WAVES", "FWD_KS",    "DKDV_WAVES", "DKDV_QS", "DQ_WAVES",        "DQ_KS",
                               "BWD_FUSED", "BWD_FUSED_DELTA", "BWD_FQS", "BWD_FKS", "BWD_FNW",
                               "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS"};
 bool known_knob(const char* k) {
@@ -81,36 +80,6 @@ int tune_knob(const char* name, int dflt) {
     for (const auto& kv : g_tune)
         if (kv.first == name) return kv.second;
     return dflt;
-}
-
-void* split_workspace(size_t bytes, hipStream_t stream) {
-    struct Ws {
-        void* p;
-        size_t n;
-    };
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, Ws> cache;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lock(mu);
-    Ws& w = cache[{dev, stream}];
-    if (w.n >= bytes) return w.p;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    // the old block may still be in use by work queued on the stream
-    if (w.p && (hipStreamSynchronize(stream) != hipSuccess || hipFree(w.p) != hipSuccess)) return nullptr;
-    w.p = nullptr;
-    w.n = 0;
-    const size_t n = std::max<size_t>(bytes, (size_t)1 << 20);
-    void* p = nullptr;
-    if (hipMalloc(&p, n) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(p, 0, n, stream) != hipSuccess) {
-        (void)hipFree(p);
-        return nullptr;
-    }
-    w.p = p;
-    w.n = n;
-    return p;
 }
 
 int cu_count() {

@@ -130,12 +130,6 @@ inline bool supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 // use it to A/B plans in one process (tools/kbench.py).
 int tune_knob(const char* name, int dflt);
 
-// Zero-initialised device workspace of at least `bytes` for launches on `stream` of the
-// current device (one per device and stream, grown on demand; kernels that use it leave
-// it zeroed).  nullptr when it would have to be allocated while `stream` is capturing,
-// or on allocation failure: the caller then takes a plan that needs none.
-void* split_workspace(size_t bytes, hipStream_t stream);
-
 // Waves per workgroup for a grid of `blocks32` 32-row wave units: the largest of
 // maxnw, maxnw/2, ..., minnw whose grid still covers every CU of the current device
 // (small problems get smaller workgroups, more of them, and waves with their SIMD

@@ -43,12 +43,10 @@ typedef short i16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 #define FA2_LOG2E 1.4426950408889634f
 #define FA2_LN2 0.6931471805599453f
-#define FA2_XS_CTRS 16384  // pair counters at the head of the split workspace
 
 // Tile element type.  The default build stores fp16 tiles.  The same source compiled
 // with -DFA2_TILE_BF16 (Makefile: *_bf16.o, namespace fa2bf16, launchers *_bf16)
@@ -476,17 +474,10 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 // each step stages KS tiles.  The groups' (m, l, O) meet in LDS after the loop
 // (O = Σ_g 2^(m_g - m) O_g, l likewise) and group 0 stores.  That puts NW waves on
 // NQ · 32 query rows, so a grid of few query blocks still covers every SIMD twice.
-//
-// XS > 1 (small grids, KS > 1 only): the key range is also split over XS workgroups
-// (consecutive blocks after the XCD remap, so a pair normally shares one L2).  Each
-// stores its merged (O, m, l) write-through into the split workspace, drains, and one
-// lane counts it in (agent-scope add; MI355X_MICROARCH §visibility, table row 1); the
-// workgroup whose add comes last resets the counter, loads every record (sc1, in
-// workgroup order, so the result does not depend on who came last) and stores O, LSE.
-template <int D, int NW, int NKB = 2, int KS = 1, int XS = 1>
+template <int D, int NW, int NKB = 2, int KS = 1>
 __global__ void __launch_bounds__(64 * NW)
 fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                   float* __restrict__ O, float* __restrict__ LSE, int S, float* __restrict__ xws) {
+                   float* __restrict__ O, float* __restrict__ LSE, int S) {
     constexpr int MQ = 1;            // query groups per wave (2 measured -30 % at D = 32/64: r01)
     constexpr bool SEED = NKB == 2;  // -m seed for 64-key tiles; 32-key tiles subtract m
     constexpr int KT = 32 * NKB;  // keys per tile
@@ -494,7 +485,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     constexpr int TILE = KT * D;
     constexpr int QW = 32 * MQ;  // query rows per wave
     static_assert(NW % KS == 0, "key split");
-    static_assert(XS == 1 || KS > 1, "cross-workgroup split only on the key-split kernels");
     constexpr int NQ = NW / KS;  // query waves (KS > 1: waves w, w + NQ, ... share rows)
     // key-split merge records: per wave of groups 1..KS-1, O (D/2 floats per lane), m, l
     constexpr int MREC = (D / 2 + 2) * 64;
@@ -512,9 +502,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     const int wave = KS > 1 ? (tid >> 6) % NQ : tid >> 6;  // query slot of the wave
     const int kg = KS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NQ) : 0;  // key group
     const int nqb = (S + QW * NQ - 1) / (QW * NQ);
-    const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
-    const int xg = XS > 1 ? bid0 % XS : 0;  // this workgroup's share of the key range
-    const int bid = XS > 1 ? bid0 / XS : bid0;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int bh = bid / nqb, qb = bid - bh * nqb;
     const long base = (long)bh * S * D;
     const int q0 = qb * QW * NQ + wave * QW + r;
@@ -529,10 +517,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     const int ntiles = (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     const int nsteps = (ntiles + KS - 1) / KS;
-    // steps [j0, j1) of the staged-step sequence (XS > 1: the workgroup's share)
-    const int xper = (nsteps + XS - 1) / XS;
-    const int j0 = XS > 1 ? min(xg * xper, nsteps) : 0;
-    const int j1 = XS > 1 ? min(j0 + xper, nsteps) : nsteps;
     // Q block (32*NQ rows, one contiguous HBM range) loaded row-coalesced, converted
     // and scaled into LDS, then read back as this wave's B fragments: 1 KB per load
     // instruction instead of 32 rows x 32 B per-lane pieces.  OVL (key split: small
@@ -545,8 +529,8 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         qst.init(Q + base, S, tid);
         qst.load(qb * QW * NQ);
         if constexpr (OVL) {
-            ks.load(j0 * KS * KT);
-            vs.load(j0 * KS * KT);
+            ks.load(0);
+            vs.load(0);
         }
         qst.store(qblk, FA2_LOG2E / __builtin_sqrtf((float)D), tid);
         if constexpr (OVL) {
@@ -582,8 +566,8 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             vs.load((j + 1) * KS * KT);
         }
         if (live) {
-            if (jj == last_ragged) fwd_softmax_pv<D, MQ, true, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h, j == j0);
-            else fwd_softmax_pv<D, MQ, false, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h, j == j0);
+            if (jj == last_ragged) fwd_softmax_pv<D, MQ, true, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h, j == 0);
+            else fwd_softmax_pv<D, MQ, false, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h, j == 0);
         }
         if (more) {
             ks.store(Kn, 1.f, tid);
@@ -592,9 +576,10 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         __syncthreads();
     };
     // two steps per trip so every LDS buffer offset is a compile-time immediate
-    for (int j = j0; j < j1; j += 2) {
-        step(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, j, j + 1 < j1);
-        if (j + 1 < j1) step(smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j + 1, j + 2 < j1);
+    for (int j = 0; j < nsteps; j += 2) {
+        step(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, j, j + 1 < nsteps);
+        if (j + 1 < nsteps)
+            step(smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j + 1, j + 2 < nsteps);
     }
     if constexpr (KS > 1) {
         // Key-split merge (the loop ended on a barrier: the tile buffers are free).
@@ -607,11 +592,11 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             for (int b = 0; b < D / 32; ++b)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) rec[(16 * b + i) * 64 + lane] = st[0].oacc[b][i];
-            rec[(D / 2) * 64 + lane] = j0 < j1 && j0 * KS + kg < ntiles ? st[0].m : -__builtin_inff();
+            rec[(D / 2) * 64 + lane] = kg < ntiles ? st[0].m : -__builtin_inff();
             rec[(D / 2 + 1) * 64 + lane] = (st[0].l[0] + st[0].l[1]) + (st[0].l[2] + st[0].l[3]);
         }
         __syncthreads();
-        if (XS == 1 && kg > 0) return;  // no workgroup barrier follows
+        if (kg > 0) return;  // no workgroup barrier follows
         float l = (st[0].l[0] + st[0].l[1]) + (st[0].l[2] + st[0].l[3]);
 #pragma unroll
         for (int g = 1; g < KS; ++g) {
@@ -628,83 +613,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         }
         st[0].l[0] = l;
         st[0].l[1] = st[0].l[2] = st[0].l[3] = 0.f;
-        // a workgroup with no step at all (XS > 1, few tiles): O = l = 0, weight 0
-        if (XS > 1 && !(j0 < j1)) st[0].m = -__builtin_inff();
-    }
-    if constexpr (XS > 1) {
-        // Cross-workgroup merge.  Record of a query wave: D/8 f32x4 of O (16-B lane
-        // pieces, [piece][lane]) and one {m, l} piece; slot [pair][xg][wave].
-        constexpr int RP = D / 8 + 1;  // 16-B pieces per lane
-        const unsigned long long wa = (unsigned long long)xws;
-        const unsigned wlo = __builtin_amdgcn_readfirstlane((unsigned)wa);
-        const unsigned whi = __builtin_amdgcn_readfirstlane((unsigned)(wa >> 32));
-        float* const wsb = (float*)(((unsigned long long)whi << 32) | wlo);
-        const int npair = __builtin_amdgcn_readfirstlane((int)(gridDim.x / XS));
-        // counters first, at fixed places (every call finds its own zeroed whatever size
-        // ran before), then the records
-        unsigned* const ctr = reinterpret_cast<unsigned*>(wsb) + bid;
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(wsb + FA2_XS_CTRS, (short)0, npair * XS * NQ * RP * 1024, 0x00020000);
-        const int slot = (bid * XS + xg) * NQ + wave;
-#ifndef FA2_XS_ABL
-        if (kg == 0) {
-#pragma unroll
-            for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const f32x4 v = {st[0].oacc[b][4 * c], st[0].oacc[b][4 * c + 1], st[0].oacc[b][4 * c + 2],
-                                     st[0].oacc[b][4 * c + 3]};
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, lane * 16,
-                                                           (slot * RP + 4 * b + c) * 1024, 16);
-                }
-            const f32x4 ml = {st[0].m, st[0].l[0], 0.f, 0.f};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ml), rs, lane * 16,
-                                                   (slot * RP + D / 8) * 1024, 16);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        int* const last = reinterpret_cast<int*>(smem);  // the merge records are read
-        if (tid == 0) {
-            const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old == XS - 1) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last[0] = old == XS - 1;
-        }
-        __syncthreads();
-        if (!last[0] || kg > 0) return;
-        // every record, in workgroup order (the last arriver's own included)
-        f32x4 rec[XS][RP];
-#pragma unroll
-        for (int x = 0; x < XS; ++x)
-#pragma unroll
-            for (int p = 0; p < RP; ++p)
-                rec[x][p] = __builtin_bit_cast(
-                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16,
-                                                                 (((bid * XS + x) * NQ + wave) * RP + p) * 1024, 16));
-        float mx = rec[0][D / 8][0];
-#pragma unroll
-        for (int x = 1; x < XS; ++x) mx = fmaxf(mx, rec[x][D / 8][0]);
-        float l = 0.f;
-#pragma unroll
-        for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) st[0].oacc[b][i] = 0.f;
-#pragma unroll
-        for (int x = 0; x < XS; ++x) {
-            const float a = fast_exp2(rec[x][D / 8][0] - mx);
-            l += rec[x][D / 8][1] * a;
-#pragma unroll
-            for (int b = 0; b < D / 32; ++b)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) st[0].oacc[b][i] += rec[x][4 * b + (i >> 2)][i & 3] * a;
-        }
-        st[0].m = mx;
-        st[0].l[0] = l;
-#else
-        (void)rs;
-        (void)ctr;
-        (void)slot;
-        if (kg > 0) return;
-#endif
     }
     // O through a wave-private LDS stage, one 32x32 block at a time, stored as whole
     // 128-B row segments (8 rows per instruction) instead of 16-B pieces of 32 rows
@@ -806,25 +714,15 @@ namespace fa2 {
 
 // KS > 1: NW / KS query waves per workgroup (D = 64: 32-key tiles -- with 64-key
 // tiles the KS-tile staging registers spill)
-template <int D, int NW, int KS = 1, int NKB = (KS == 1 || D <= 32 ? 2 : 1), int XS = 1>
+template <int D, int NW, int KS = 1, int NKB = (KS == 1 || D <= 32 ? 2 : 1)>
 static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
-                                 hipStream_t stream, float* xws = nullptr) {
+                                 hipStream_t stream) {
     const int nqb = (S + 32 * (NW / KS) - 1) / (32 * (NW / KS));
-    const long grid = (long)bh * nqb * XS;
+    const long grid = (long)bh * nqb;
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, NKB, KS, XS>), dim3((unsigned)grid), dim3(64 * NW), 0, stream,
-                       q, k, v, o, lse, S, xws);
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_f16_kernel<D, NW, NKB, KS>), dim3((unsigned)grid), dim3(64 * NW), 0, stream, q, k,
+                       v, o, lse, S);
     return hipGetLastError();
-}
-
-// Split workspace of the XS = 2 forward: FA2_XS_CTRS pair counters (zeroed at
-// allocation, reset by each pair's last workgroup), then per pair XS records of NQ
-// waves x (D/8 + 1) x 1 KiB.  0 when the grid has more pairs than counters.
-template <int D, int NW, int KS, int XS>
-static size_t fwd_xs_bytes(int bh, int S) {
-    const long npair = (long)bh * ((S + 32 * (NW / KS) - 1) / (32 * (NW / KS)));
-    if (npair > FA2_XS_CTRS) return 0;
-    return (size_t)FA2_XS_CTRS * 4 + (size_t)npair * XS * (NW / KS) * (D / 8 + 1) * 1024;
 }
 
 template <int D>
@@ -857,13 +755,6 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     }
     if (nw == 0) nw = auto_waves(units, 8);
     if constexpr (D <= 64) {
-        // FWD_XS = 2: the KS = 4, 8-wave kernel with the key range also split over two
-        // workgroups (r03 experiment, off by default: DESIGN.md §3 "Small grids")
-        if (ks == 4 && nw == 8 && tune_knob("FWD_XS", 1) == 2) {
-            const size_t bytes = fwd_xs_bytes<D, 8, 4, 2>(bh, S);
-            if (float* ws = bytes ? static_cast<float*>(split_workspace(bytes, stream)) : nullptr)
-                return fwd_f16_launch<D, 8, 4, 1, 2>(q, k, v, o, lse, bh, S, stream, ws);
-        }
         if (ks == 2 && nw == 8) return fwd_f16_launch<D, 8, 2>(q, k, v, o, lse, bh, S, stream);
         if (ks == 4 && nw == 8) return fwd_f16_launch<D, 8, 4>(q, k, v, o, lse, bh, S, stream);
         if (ks == 4 && nw == 4) return fwd_f16_launch<D, 4, 4>(q, k, v, o, lse, bh, S, stream);
