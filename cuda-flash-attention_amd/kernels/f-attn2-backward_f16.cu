@@ -414,13 +414,25 @@ struct FragOffsets16 {
     }
 };
 
-template <int D, typename Mid>
+// LLVM scheduling strategies (__builtin_amdgcn_iglp_opt) for the unsplit dK/dV and dQ
+// kernels' step bodies at D = 64; -1 = the default scheduler.  r03, in-process A/Bs
+// (`profiles/r03/ab/iglp/`): strategy 0 on dK/dV -1.3 % at C3 in three runs (step -0.6 %,
+// C5 and B2_H8_S4096 -0.5 %), +12 % slower at D = 32 (so D = 64 only); strategies 1-3
+// and any strategy on dQ within +-0.8 %.
+#ifndef FA2_IGLP_DKDV
+#define FA2_IGLP_DKDV 0
+#endif
+#ifndef FA2_IGLP_DQ
+#define FA2_IGLP_DQ -1
+#endif
+template <int D, int IGLP = -1, typename Mid>
 __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
                                             const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
                                             int g, Mid&& mid) {
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
         if (qb == 1) mid();
+        if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);  // LLVM scheduling strategy for the region
         f32x4 sa[2][2], da[2][2];  // [mb][nb]
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb) {
@@ -524,7 +536,7 @@ struct DkdvLds {
 // the BH * ceil(S / (KPW * NK)) key blocks.
 // DEL: Δ = rowsum(dO ∘ O) of every staged step computed here from O rows staged
 // beside dO (no Delta input: the fused small-grid launch, whose dQ role writes Δ).
-template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1, bool DEL = false>
+template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1, bool DEL = false, int IGLP = -1>
 __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const float* __restrict__ Q,
                                           const float* __restrict__ K, const float* __restrict__ V,
                                           const float* __restrict__ dO, const float* __restrict__ LSE,
@@ -710,7 +722,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         if constexpr (M16) {
             const bool live = QS == 1 || itc * QS + qg < nqt;  // wave-uniform
             if (!live) mid();
-            else dkdv_step16<D>(st16, Qb, dOb, r0 + rq, r1 + rq, fo16, g16, mid);
+            else dkdv_step16<D, IGLP>(st16, Qb, dOb, r0 + rq, r1 + rq, fo16, g16, mid);
         } else {
             dkdv_step<D, KB>(st, Qb, dOb, r0, r1, fo, h, mid);
         }
@@ -786,7 +798,9 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
                         const float* __restrict__ dO, const float* __restrict__ LSE,
                         const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV, int S) {
     __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, KB, QS>::BYTES];
-    dkdv_body<D, NW, KB, M16, QS>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE, Delta, dK, dV, S);
+    // the unsplit instances (full grids: C3, C5, long S) under an LLVM scheduling strategy
+    dkdv_body<D, NW, KB, M16, QS, false, QS == 1 && D == 64 ? FA2_IGLP_DKDV : -1>(lds, xcd_remap(blockIdx.x, gridDim.x),
+                                                                                 Q, K, V, dO, LSE, Delta, dK, dV, S);
 }
 
 // ---------------------------------------------------------------------------
@@ -844,13 +858,14 @@ struct DqState16 {
     f32x4 nlse2[2], ndel[2];             // [nb]: splats of the lane's -lse2 / -delta
 };
 
-template <int D, bool MASK, int NKB, typename Mid>
+template <int D, bool MASK, int NKB, int IGLP = -1, typename Mid>
 __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, const _Float16* Vs,
                                           const FragOffsets16<D>& fo, int k0, int S, int g, Mid&& mid) {
     f16x8 dsf[NKB][2];  // [32-key half kb][nb]
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
         if (NKB > 1 && kb == 1) mid();  // the next tile's loads between the two 32-key halves
+        if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);  // LLVM scheduling strategy for the region
         f32x4 sa[2][2], da[2][2];  // [mbl][nb]: keys k0 + 32 kb + 16 mbl + 4g + i
 #pragma unroll
         for (int mbl = 0; mbl < 2; ++mbl)
@@ -924,7 +939,7 @@ struct DqLds {
 
 // One workgroup of the dQ kernel; `bid` is its (XCD-remapped) block number over the
 // BH * ceil(S / (32 * NQ)) query blocks.
-template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1>
+template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1, int IGLP = -1>
 __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const float* __restrict__ Q,
                                         const float* __restrict__ K, const float* __restrict__ V,
                                         const float* __restrict__ dO, const float* __restrict__ LSE,
@@ -1082,8 +1097,9 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
             auto mid = [&] { ld(); };  // also on the last step (see FA2_DKDV_SW's note)
             if constexpr (M16) {
                 if (!live) mid();
-                else if (jj == last_ragged) dq_tile16<D, true, NKB>(st16, smem, smem + KS * TILE, fo16, jj * KT, S, g16, mid);
-                else dq_tile16<D, false, NKB>(st16, smem, smem + KS * TILE, fo16, jj * KT, S, g16, mid);
+                else if (jj == last_ragged)
+                    dq_tile16<D, true, NKB, IGLP>(st16, smem, smem + KS * TILE, fo16, jj * KT, S, g16, mid);
+                else dq_tile16<D, false, NKB, IGLP>(st16, smem, smem + KS * TILE, fo16, jj * KT, S, g16, mid);
             } else {
                 if (j == last_ragged) dq_tile<D, true, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
                 else dq_tile<D, false, NKB>(st, smem, smem + TILE, fo, j * KT, S, h, mid);
@@ -1106,9 +1122,10 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
             if constexpr (M16) {
                 if (!live) mid();
                 else if (jj == last_ragged)
-                    dq_tile16<D, true, NKB>(st16, smem + 2 * KS * TILE, smem + 3 * KS * TILE, fo16, jj * KT, S, g16, mid);
-                else dq_tile16<D, false, NKB>(st16, smem + 2 * KS * TILE, smem + 3 * KS * TILE, fo16, jj * KT, S, g16,
-                                              mid);
+                    dq_tile16<D, true, NKB, IGLP>(st16, smem + 2 * KS * TILE, smem + 3 * KS * TILE, fo16, jj * KT, S, g16,
+                                                  mid);
+                else dq_tile16<D, false, NKB, IGLP>(st16, smem + 2 * KS * TILE, smem + 3 * KS * TILE, fo16, jj * KT, S,
+                                                    g16, mid);
             } else {
                 if (j + 1 == last_ragged)
                     dq_tile<D, true, NKB>(st, smem + 2 * TILE, smem + 3 * TILE, fo, (j + 1) * KT, S, h, mid);
@@ -1165,7 +1182,8 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
                       const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
                       float* __restrict__ dQ, int S, const float* __restrict__ O) {
     __shared__ __attribute__((aligned(16))) char lds[DqLds<D, NW, DELTA, NKB, KS>::BYTES];
-    dq_body<D, NW, DELTA, NKB, M16, KS>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE, Delta, dQ, S, O);
+    dq_body<D, NW, DELTA, NKB, M16, KS, KS == 1 && D == 64 ? FA2_IGLP_DQ : -1>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K,
+                                                                              V, dO, LSE, Delta, dQ, S, O);
 }
 
 // dK/dV and dQ in ONE launch (small grids).  Workgroups [0, ndk) take the dK/dV role
