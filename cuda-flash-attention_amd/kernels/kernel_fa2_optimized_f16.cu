@@ -272,6 +272,14 @@ struct FwdState {
 // path keeps is therefore <= 2^13: exact-range fp16 for the PV operand.
 #define FA2_TILE_SUM_MAX 8192.0f
 
+// LLVM scheduling strategy (__builtin_amdgcn_iglp_opt) for the QK^T and PV regions at
+// D = 128; -1 = the default scheduler.  r03 in-process A/Bs (`profiles/r03/ab/figlp/`):
+// strategy 0 took C4 (B8_H16_S4096_D128) 1.2-1.5 % faster in two runs, D = 128 at S = 2048
+// +-0; at D = 64 every strategy (0-3) lost 5 % at C3, so D = 64 keeps the default.
+#ifndef FA2_FWD_IGLP
+#define FA2_FWD_IGLP 0
+#endif
+
 // -m as one opaque 16-register tuple: without the empty asm the compiler
 // rematerialises the splat with 16 v_mov before every QK^T chain.
 __device__ __forceinline__ f32x16 splat16(float x) {
@@ -287,6 +295,7 @@ __device__ __forceinline__ f32x16 splat16(float x) {
 template <int D, int MQ, int NKB = 2, bool SEED = true>
 __device__ __forceinline__ void fwd_qk(f32x16 (&s)[MQ][NKB], const FwdState<D> (&st)[MQ], const _Float16* Ks,
                                        const FragOffsets<D>& fo) {
+    if constexpr (D == 128 && FA2_FWD_IGLP >= 0) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP);
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
         const f16x8 a0 = fo.rowop(Ks, kb * 32, 0);
@@ -363,6 +372,7 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
     // audit: 29 v_mov per 64-key tile at D = 64; 32 v_mov_b64 + 5 v_mov_b32 per 32-key
     // tile at D = 128); joined after it, the merged values are MFMA results.
     auto accumulate = [&]() {
+        if constexpr (D == 128 && FA2_FWD_IGLP >= 0) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP);
 #pragma unroll
         for (int g = 0; g < MQ; ++g)
 #pragma unroll
