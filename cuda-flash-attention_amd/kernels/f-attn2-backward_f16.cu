@@ -425,14 +425,25 @@ struct FragOffsets16 {
 #ifndef FA2_IGLP_DQ
 #define FA2_IGLP_DQ -1
 #endif
+// ... and for both roles of the fused small-grid backward: strategy 2 took B2_H8_S512
+// 15.8 -> 15.3 us (dO = ones) and 15.6 -> 15.1 (N(0,1)), S = 1024 fwd + bwd -1.5 %,
+// B4_H8_S512, D = 32 and S = 2048 +-0; strategy 1 lost 4 % at S = 512
+#ifndef FA2_IGLP_FUSED
+#define FA2_IGLP_FUSED 2
+#endif
 template <int D, int IGLP = -1, typename Mid>
 __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
                                             const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
                                             int g, Mid&& mid) {
+#ifdef FA2_IGLP_DKDV_ONCE
+    if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
+#endif
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
         if (qb == 1) mid();
+#ifndef FA2_IGLP_DKDV_ONCE
         if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);  // LLVM scheduling strategy for the region
+#endif
         f32x4 sa[2][2], da[2][2];  // [mb][nb]
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb) {
@@ -1208,10 +1219,10 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
     __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
     const int b = blockIdx.x;
     if (b < ndk)
-        dkdv_body<D, NW, 1, true, QS, DEL>(lds, xcd_remap(b, ndk), Q, K, V, dO, LSE, Delta, dK, dV, S, O);
+        dkdv_body<D, NW, 1, true, QS, DEL, FA2_IGLP_FUSED>(lds, xcd_remap(b, ndk), Q, K, V, dO, LSE, Delta, dK, dV, S, O);
     else
-        dq_body<D, NW, DEL, NKB, true, KS>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE, Delta, dQ, S,
-                                           O);
+        dq_body<D, NW, DEL, NKB, true, KS, FA2_IGLP_FUSED>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
+                                                           Delta, dQ, S, O);
 }
 
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),

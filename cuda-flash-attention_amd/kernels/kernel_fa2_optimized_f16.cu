@@ -296,6 +296,9 @@ template <int D, int MQ, int NKB = 2, bool SEED = true>
 __device__ __forceinline__ void fwd_qk(f32x16 (&s)[MQ][NKB], const FwdState<D> (&st)[MQ], const _Float16* Ks,
                                        const FragOffsets<D>& fo) {
     if constexpr (D == 128 && FA2_FWD_IGLP >= 0) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP);
+#ifdef FA2_FWD_IGLP_QK64
+    if constexpr (D == 64) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP_QK64);
+#endif
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
         const f16x8 a0 = fo.rowop(Ks, kb * 32, 0);
@@ -373,6 +376,9 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
     // tile at D = 128); joined after it, the merged values are MFMA results.
     auto accumulate = [&]() {
         if constexpr (D == 128 && FA2_FWD_IGLP >= 0) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP);
+#ifdef FA2_FWD_IGLP_PV64
+        if constexpr (D == 64) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP_PV64);
+#endif
 #pragma unroll
         for (int g = 0; g < MQ; ++g)
 #pragma unroll
