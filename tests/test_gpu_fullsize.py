@@ -238,3 +238,38 @@ def test_host_api_shards_on_one_device_small(chunks):
                 assert maxerr(got, exp) < tol * max(1.0, float(np.abs(exp).max())), precision
     finally:
         fa2amd.tune_set(None)
+
+
+# ---------------------------------------------------------------------------
+# Beyond 2^31 elements per tensor: 64-bit offsets everywhere on the path
+# ---------------------------------------------------------------------------
+def test_tensors_beyond_int32_elements():
+    """B1_H4104_S8192_D64: 2.15e9 elements (8.6 GB) per tensor, more than a 32-bit index
+    reaches (the reference's own CLI keeps sizes in int, src/main.cpp:27).  fwd + bwd on
+    one GPU (inputs drawn on the device, dO = ones); the first, a middle and the last head
+    (whose rows start past element 2^31) against the C oracle, every tensor finite."""
+    if torch.cuda.get_device_properties(0).total_memory < 100 * 2**30:
+        pytest.skip("needs ~70 GB of device memory")
+    B, H, S, D = 1, 4104, 8192, 64
+    assert B * H * S * D > 2**31
+    g = torch.Generator(device="cuda").manual_seed(7)
+    q, k, v = (torch.rand(B, H, S, D, device="cuda", generator=g) for _ in range(3))
+    ones = torch.ones_like(q)
+    o, lse = fa2amd.forward(q, k, v, "fp16")
+    dq, dk, dv = fa2amd.backward(q, k, v, o, ones, lse, "fp16")
+    torch.cuda.synchronize()
+    for name, t in (("o", o), ("lse", lse), ("dq", dq), ("dk", dk), ("dv", dv)):
+        assert bool(torch.isfinite(t).all()), name
+    idx = [0, H // 2, H - 1]
+    sel = lambda t: np.ascontiguousarray(t[0, idx].cpu().numpy())[None]  # noqa: E731
+    hq, hk, hv = sel(q), sel(k), sel(v)
+    go, gl, gdq, gdk, gdv = sel(o), sel(lse), sel(dq), sel(dk), sel(dv)
+    del q, k, v, ones, o, lse, dq, dk, dv
+    torch.cuda.empty_cache()
+    eo, el = c_oracle.forward(hq, hk, hv, NT)
+    h1 = np.ones_like(hq)
+    edq, edk, edv = c_oracle.backward(hq, hk, hv, eo, h1, el, NT)
+    assert maxerr(go, eo) < TOL["fp16"] and maxerr(gl, el) < TOL["fp16"]
+    got = np.concatenate([x.ravel() for x in (gdq, gdk, gdv)])
+    assert maxerr(got, np.concatenate([x.ravel() for x in (edq, edk, edv)])) < TOL["fp16"]
+    assert_identities(hq, hv, h1, go, gdk, gdv)
