@@ -1559,7 +1559,7 @@ hipError_t fused_launch(const float* q, const float* k, const float* v, const fl
     return hipGetLastError();
 }
 // The fused dK/dV + dQ launch for D <= 64, or hipErrorNotSupported (then the caller
-// runs the two kernels).  Split factors: below 8 blocks of 32 rows per CU QS = 2 /
+// runs the two kernels).  Split factors: below 4 blocks of 32 rows per CU QS = 2 /
 // KS = 2, else unsplit.  Overrides (fa2_tune_set): BWD_FQS, BWD_FKS, BWD_FNW.
 template <int D>
 hipError_t fused_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
@@ -1576,8 +1576,12 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
         // dQ role KS = 2 on every split grid (r02: below 4 blocks per CU KS = 2 beat the
         // r01 choice KS = 4 by 4.6-7.5 % on the fwd + bwd step, B2_H8_S1024 D = 32 / 64,
         // B4_H8_S512, B1_H16_S1024, S = 1000, both dO distributions)
-        const int fqs = tune_knob("BWD_FQS", a == 8 ? 1 : 2);
-        const int fks = tune_knob("BWD_FKS", a == 8 ? 1 : 2);
+        // With 4-8 blocks per CU both roles run unsplit (r03, with iglp_opt(2) on the
+        // fused kernel: B2_H8_S2048 bwd 69.0 -> 64.4 us, dO ~ N(0,1) 72.7 -> 68.0, S = 1500
+        // 54.3 -> 48.7, B4_H8_S1024 43.9 -> 39.6, D = 32 S = 2048 44.3 -> 41.6;
+        // profiles/r03/ab/froles/); below 4 the split roles stay (S = 1024: 24.6 vs 33.4)
+        const int fqs = tune_knob("BWD_FQS", a >= 4 ? 1 : 2);
+        const int fks = tune_knob("BWD_FKS", a >= 4 ? 1 : 2);
         // waves per workgroup of both roles (8, or 4 for the split pairs)
         const int fnw = tune_knob("BWD_FNW", tiny ? 4 : 8);
         if (fqs == 1 && fks == 1) return fused_launch<D, 8, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
