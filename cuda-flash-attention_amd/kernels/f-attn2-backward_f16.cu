@@ -425,9 +425,11 @@ struct FragOffsets16 {
 #ifndef FA2_IGLP_DQ
 #define FA2_IGLP_DQ -1
 #endif
-// ... and for both roles of the fused small-grid backward: strategy 2 took B2_H8_S512
-// 15.8 -> 15.3 us (dO = ones) and 15.6 -> 15.1 (N(0,1)), S = 1024 fwd + bwd -1.5 %,
-// B4_H8_S512, D = 32 and S = 2048 +-0; strategy 1 lost 4 % at S = 512
+// ... and for the fused small-grid backward: strategy 2 took B2_H8_S512 15.8 -> 15.3 us
+// (dO = ones) and 15.6 -> 15.1 (N(0,1)), S = 1024 fwd + bwd -1.5 %, B4_H8_S512, D = 32
+// and S = 2048 +-0; strategy 1 lost 4 % at S = 512.  Per role: the dK/dV role needs it
+// with split queries (S = 512: 16.0 us without), and with unsplit queries (4-8 blocks per
+// CU) strategy 0 is better (B2_H8_S2048 64.4 -> 62.7 us); the dQ role +-1 % either way.
 #ifndef FA2_IGLP_FUSED
 #define FA2_IGLP_FUSED 2
 #endif
@@ -1219,7 +1221,9 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
     __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
     const int b = blockIdx.x;
     if (b < ndk)
-        dkdv_body<D, NW, 1, true, QS, DEL, FA2_IGLP_FUSED>(lds, xcd_remap(b, ndk), Q, K, V, dO, LSE, Delta, dK, dV, S, O);
+        // the dK/dV role with unsplit queries takes the standalone kernel's strategy
+        dkdv_body<D, NW, 1, true, QS, DEL, QS == 1 && D == 64 ? FA2_IGLP_DKDV : FA2_IGLP_FUSED>(
+            lds, xcd_remap(b, ndk), Q, K, V, dO, LSE, Delta, dK, dV, S, O);
     else
         dq_body<D, NW, DEL, NKB, true, KS, FA2_IGLP_FUSED>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
                                                            Delta, dQ, S, O);
