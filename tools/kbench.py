@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", action="append", default=[], help="alternate libfa2amd.so builds to A/B (repeatable)")
     ap.add_argument("--do", choices=["randn", "ones"], default="randn", help="dO distribution (bench.py uses ones)")
+    ap.add_argument("--precision", choices=["fp16", "bf16", "fp32"], default="fp16",
+                    help="tile precision of the fwd / bwd / stepb calls")
     args = ap.parse_args()
     import torch
     import fa2amd
@@ -33,7 +35,8 @@ def main():
     g = torch.Generator().manual_seed(42)
     q, k, v = (torch.rand(B, H, S, D, generator=g).to(dev) for _ in range(3))
     do = torch.randn(B, H, S, D, generator=g).to(dev) if args.do == "randn" else torch.ones(B, H, S, D, device=dev)
-    o, lse = fa2amd.forward(q, k, v, "fp16")
+    P = args.precision
+    o, lse = fa2amd.forward(q, k, v, P)
     dl = fa2amd.delta(do, o)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
     flops = {"fwd": 4.0, "dkdv": 8.0, "dq": 2.0, "dqd": 2.0, "delta": 0.0, "bwd": 10.0, "step": 14.0, "stepb": 14.0,
@@ -58,19 +61,19 @@ def main():
         ev2.record(s2)
         cur.wait_event(ev2)
     calls = {
-        "fwd": lambda: fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
+        "fwd": lambda: fa2amd.forward(q, k, v, P, out=o, lse=lse),
         "dkdv": lambda: fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv),
         "dq": lambda: fa2amd.backward_dq(q, k, v, do, lse, dl, dq),
         "delta": lambda: fa2amd.delta(do, o, out=dl),
-        "bwd": lambda: fa2amd.backward(q, k, v, o, do, lse, "fp16", dq=dq, dk=dk, dv=dv, delta_buf=dl),
+        "bwd": lambda: fa2amd.backward(q, k, v, o, do, lse, P, dq=dq, dk=dk, dv=dv, delta_buf=dl),
         # one bench.py step: fwd, delta, dK/dV, dQ in stream order
         "step": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
                          fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
                          fa2amd.backward_dkdv(q, k, v, do, lse, dl, dk, dv)),
         "dqd": lambda: fa2amd.backward_dq_delta(q, k, v, o, do, lse, dl, dq),
         # fwd + fa2_backward (whatever launch plan launch_backward picks, e.g. BWD_FUSED)
-        "stepb": lambda: (fa2amd.forward(q, k, v, "fp16", out=o, lse=lse),
-                          fa2amd.backward(q, k, v, o, do, lse, "fp16", dq=dq, dk=dk, dv=dv, delta_buf=dl)),
+        "stepb": lambda: (fa2amd.forward(q, k, v, P, out=o, lse=lse),
+                          fa2amd.backward(q, k, v, o, do, lse, P, dq=dq, dk=dk, dv=dv, delta_buf=dl)),
         # dK/dV and dQ on two streams after a separate delta kernel
         "step2s": lambda: two_stream_step(True),
         "step2r": lambda: two_stream_step(False),
