@@ -393,9 +393,15 @@ int run_shard(HostJob& j) {
             out_err = g_err;
         }
     });
+    // error exits: no copy may still read or write the caller's host buffers, nor
+    // the pool's device memory, once the pool lock is released and the call returns
+    auto drain = [&] {
+        for (hipStream_t s : {r.si, r.sc, r.so}) (void)hipStreamSynchronize(s);
+    };
     auto stop = [&](int code) {
         abort.store(true, std::memory_order_release);
         d2h.join();
+        drain();
         return code;
     };
     for (int c = 0; c < nch; ++c) {
@@ -426,7 +432,10 @@ int run_shard(HostJob& j) {
         issued.store(c + 1, std::memory_order_release);
     }
     d2h.join();
-    if (out_rc) return fail(out_rc, out_err);
+    if (out_rc) {
+        drain();
+        return fail(out_rc, out_err);
+    }
     if ((rc = hip_status(hipStreamSynchronize(r.sc), "kernel"))) return rc;
     float ms = 0.f;
     for (int c = 0; c < nch; ++c) {
