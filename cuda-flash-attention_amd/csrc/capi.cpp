@@ -65,7 +65,7 @@ std::atomic<int> g_tune_n{0};
 // so a misspelt knob cannot silently leave an A/B on the default plan)
 const char* const kKnobs[] = {"FWD_WAVES", "FWD_KS",    "DKDV_WAVES", "DKDV_QS", "DQ_WAVES",        "DQ_KS",
                               "BWD_FUSED", "BWD_FUSED_DELTA", "BWD_FQS", "BWD_FKS", "BWD_FNW",
-                              "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS", "DKDV_PERSIST"};
+                              "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS"};
 bool known_knob(const char* k) {
     for (const char* n : kKnobs)
         if (!strcmp(n, k)) return true;

@@ -197,9 +197,8 @@ struct TileStager {
     __amdgpu_buffer_rsrc_t rs;
     bool on = true;  // wave-uniform: this wave takes part in the staging
 
-    __device__ __forceinline__ void set_head(const float* head_base, int S) { rs = head_rsrc(head_base, S, D); }
     __device__ __forceinline__ void init(const float* head_base, int S, int tid) {
-        set_head(head_base, S);
+        rs = head_rsrc(head_base, S, D);
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
             const int x = tid + c * NT;
@@ -550,17 +549,12 @@ struct DkdvLds {
 // the BH * ceil(S / (KPW * NK)) key blocks.
 // DEL: Δ = rowsum(dO ∘ O) of every staged step computed here from O rows staged
 // beside dO (no Delta input: the fused small-grid launch, whose dQ role writes Δ).
-// PERSIST (QS = 1): the workgroup walks key blocks start_x + w, + G/8, ... of its XCD's
-// contiguous range (grid G, a multiple of 8, WG b on XCD b % 8); the next block's K and
-// V loads are issued before this block's dK/dV stores, so they overlap in HBM.
-template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1, bool DEL = false, int IGLP = -1,
-          bool PERSIST = false>
+template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1, bool DEL = false, int IGLP = -1>
 __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const float* __restrict__ Q,
                                           const float* __restrict__ K, const float* __restrict__ V,
                                           const float* __restrict__ dO, const float* __restrict__ LSE,
                                           const float* __restrict__ Delta, float* __restrict__ dK,
-                                          float* __restrict__ dV, int S, const float* __restrict__ O = nullptr,
-                                          int nblk = 0) {
+                                          float* __restrict__ dV, int S, const float* __restrict__ O = nullptr) {
     using L = DkdvLds<D, NW, KB, QS>;
     constexpr int QT = L::QT;  // query rows per step
     constexpr int NT = 64 * NW;
@@ -576,32 +570,11 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
     const int wave = QS > 1 ? (tid >> 6) % NK : tid >> 6;  // key slot of the wave
     const int qg = QS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NK) : 0;  // query group
     const int nkb = (S + KPW * NK - 1) / (KPW * NK);
-    static_assert(!PERSIST || QS == 1, "persistent walk: unsplit queries");
-    int pidx = 0, pcnt = 1, pstart = 0;
-    constexpr int PSTEP_SHIFT = 3;  // workers per XCD = gridDim.x >> 3
-    if constexpr (PERSIST) {
-        const int x = blockIdx.x & 7, q8 = nblk >> 3, r8 = nblk & 7;
-        pcnt = q8 + (x < r8 ? 1 : 0);
-        pstart = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
-        pidx = blockIdx.x >> 3;
-        if (pidx >= pcnt) return;  // the whole workgroup: no barrier reached
-        bid = pstart + pidx;
-    }
-    const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
-    TileStager<D, KPW * NK, NT> kst, vst;
-    if constexpr (PERSIST) {  // the first block's K and V loads (later blocks': below)
-        const long base0 = (long)(bid / nkb) * S * D;
-        const int kb0 = (bid - (bid / nkb) * nkb) * KPW * NK;
-        kst.init(K + base0, S, tid);
-        vst.init(V + base0, S, tid);
-        kst.load(kb0);
-        vst.load(kb0);
-    }
-  for (;;) {
     const int bh = bid / nkb, kblk = bid - bh * nkb;
     const long base = (long)bh * S * D;
     const long rbase = (long)bh * S;
     const int key0 = kblk * KPW * NK + wave * KPW;  // this wave's first key
+    const float kscale = FA2B_LOG2E / __builtin_sqrtf((float)D);
 
     DkdvState<D, KB> st;
     FragOffsets<D> fo;
@@ -644,18 +617,17 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
                 for (int t = 0; t < D / 16; ++t) st.vf[kb][t] = fo.rowop(vblk, wave * KPW + kb * 32, t);
         }
     };
-    if constexpr (!PERSIST) {
-        kst.init(K + base, S, tid);
-        vst.init(V + base, S, tid);
-        kst.load(kblock0);
-    }
+    TileStager<D, KPW * NK, NT> kst, vst;
+    kst.init(K + base, S, tid);
+    vst.init(V + base, S, tid);
+    kst.load(kblock0);
     if constexpr (!L::OVL) {
         kst.store(smem, kscale, tid);
         __syncthreads();
         read_k();
         __syncthreads();
     }
-    if constexpr (!PERSIST) vst.load(kblock0);
+    vst.load(kblock0);
     if constexpr (!L::OVL) {
         vst.store(smem, 1.f, tid);
         __syncthreads();
@@ -819,24 +791,6 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
                     }
         }
     }
-    // PERSIST: the next block's K / V loads go out before this block's stores
-    int nxt = -1;
-    if constexpr (PERSIST) {
-        pidx += gridDim.x >> PSTEP_SHIFT;
-        if (pidx < pcnt) {
-            nxt = __builtin_amdgcn_readfirstlane(pstart + pidx);
-            const int nbh = nxt / nkb;
-            const long nbase = (long)nbh * S * D;
-            const int nkb0 = (nxt - nbh * nkb) * KPW * NK;
-            // offsets recomputed here: kept live across the step loop they spilled
-            int t = tid;
-            asm volatile("" : "+v"(t));  // opaque: the offsets are not hoisted out of the walk
-            kst.init(K + nbase, S, t);
-            vst.init(V + nbase, S, t);
-            kst.load(nkb0);
-            vst.load(nkb0);
-        }
-    }
     const float dscale = 1.f / __builtin_sqrtf((float)D);
     if constexpr (M16) {
         store_block_rows16<D>(ostage[wave], st16.dka, dscale, dK + base + (long)key0 * D, S - key0, lane);
@@ -849,9 +803,6 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
             store_block_rows<D>(ostage[wave], st.dva[kb], 1.f, dV + base + (long)k0r * D, S - k0r, lane);
         }
     }
-    if (!PERSIST || nxt < 0) break;
-    bid = nxt;
-  }
 }
 
 template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1>
@@ -863,19 +814,6 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     // the unsplit instances (full grids: C3, C5, long S) under an LLVM scheduling strategy
     dkdv_body<D, NW, KB, M16, QS, false, QS == 1 && D == 64 ? FA2_IGLP_DKDV : -1>(lds, xcd_remap(blockIdx.x, gridDim.x),
                                                                                  Q, K, V, dO, LSE, Delta, dK, dV, S);
-}
-
-// Persistent instance (DKDV_PERSIST): grid G (a multiple of 8, at most one workgroup
-// per CU) walking nblk = BH * ceil(S / (32 * NW)) key blocks.
-template <int D, int NW>
-__global__ void __launch_bounds__(64 * NW)
-fa2_bwd_dkdv_f16_pkernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                         const float* __restrict__ dO, const float* __restrict__ LSE,
-                         const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV, int S,
-                         int nblk) {
-    __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, 1, 1>::BYTES];
-    dkdv_body<D, NW, 1, true, 1, false, D == 64 ? FA2_IGLP_DKDV : -1, true>(lds, 0, Q, K, V, dO, LSE, Delta, dK, dV, S,
-                                                                           nullptr, nblk);
 }
 
 // ---------------------------------------------------------------------------
@@ -1510,17 +1448,6 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
         else if (a == 2) qs = 2, nw = 4;
     }
     if (nw == 0) nw = auto_waves(units, D <= 64 ? 8 : 4);
-    if constexpr (D == 64) {
-        // persistent walk (A/B knob): one workgroup per CU over more than one round of blocks
-        const long nblk = (long)bh * ((S + 255) / 256);
-        const int pm = tune_knob("DKDV_PERSIST", 0);  // 2: the same kernel, one block per workgroup (A/B)
-        const int g = pm == 2 ? (int)(nblk & ~7L) : cu_count() & ~7;
-        if (pm && qs <= 1 && nw == 8 && g >= 8 && (nblk > g || pm == 2) && nblk <= 0x7fffffffL) {
-            hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_f16_pkernel<D, 8>), dim3((unsigned)g), dim3(512), 0, stream, q, k,
-                               v, dout, lse, delta, dk, dv, S, (int)nblk);
-            return hipGetLastError();
-        }
-    }
     if constexpr (D <= 64) {
         if (qs == 2 && nw == 8) return dkdv_launch<D, 8, true, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
         if (qs == 2 && nw == 4) return dkdv_launch<D, 4, true, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);

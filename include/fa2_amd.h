@@ -126,8 +126,7 @@ int fa2_shard_range(int total_heads, int shards, int index, int* first, int* cou
  * environment).  fa2_tune_set("DKDV_QS", 2) makes the next launches use that plan
  * where the shape allows it; fa2_tune_set(NULL, 0) clears every override.  Knobs:
  * FWD_WAVES, FWD_KS, DKDV_WAVES, DKDV_QS, DQ_WAVES, DQ_KS, BWD_FUSED,
- * BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW, DKDV_PERSIST (see the launchers in
- * kernels/), and
+ * BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW (see the launchers in kernels/), and
  * the test-only HOST_SHARDS_ON_DEVICE0 = 1 (fa2_*_host run every shard on device 0,
  * so an N-way split's head offsets are testable on one GPU) and HOST_CHUNKS (head
  * chunks of the fa2_*_host pipeline; 0 = auto).  Any other name:
