@@ -269,9 +269,9 @@ struct FwdState {
 // computes p = exp2(s - m) and the tile's row sum straight away; a half-row sum
 // above 2^13 (or inf / NaN) sends the whole wave to the slow path, which takes the
 // row max, moves m, rescales l and O and recomputes the tile.  Every p the common
-// path keeps is therefore <= 2^13: exact-range fp16 for the PV operand.  With an
-// unsplit key range (KS = 1) the loop runs the common path only, and a block where any
-// wave saw such a sum is redone from its first tile by the loop with the slow path.
+// path keeps is therefore <= 2^13: exact-range fp16 for the PV operand.  The
+// library kernel's tile loop runs the common path only; a block where any wave saw
+// such a sum is redone from its first tile by the loop with the slow path.
 #define FA2_TILE_SUM_MAX 8192.0f
 
 // LLVM scheduling strategy (__builtin_amdgcn_iglp_opt) for the QK^T and PV regions at
@@ -644,23 +644,29 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                 step(smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j + 1, j + 2 < nsteps);
         }
     };
-    // Unsplit key range: tile 0 sets m (the rescaling step); tiles 1.. run the
+    // Tile 0 (each key group's first) sets m (the rescaling step); tiles 1.. run the
     // branch-free common path and only note a sum out of range; if any wave noted one,
     // the whole workgroup restarts the block with the rescaling loop (late score spikes
     // only).  Without the rescale branch in the loop the register allocator keeps O, l
-    // and -m in place: r03, in-process A/B, C3 step -1.4 %, C4 forward -2.1 %, the
-    // S = 4096 forward -1.7 %.
-    if constexpr (KS == 1) {
+    // and -m in place: r03, in-process A/Bs (profiles/r03/ab/fast/): forward -1.2 ..
+    // -1.9 % at C3, C4, C5 and B2_H8_S4096; key-split grids (B2_H8, S = 512 - 2048)
+    // fwd + bwd step -1 .. -2 %.
+    constexpr bool FWD_FAST = true;
+    if constexpr (FWD_FAST) {
         auto stepf = [&](const _Float16* Kc, const _Float16* Vc, _Float16* Kn, _Float16* Vn, int j, bool more)
             __attribute__((always_inline)) {
+            const int jj = j * KS + kg;                // this wave's tile
+            const bool live = KS == 1 || jj < ntiles;  // wave-uniform (KS > 1: ragged tail)
             f32x16 sacc[MQ][NKB];
-            fwd_qk<D, MQ, NKB, SEED>(sacc, st, Kc, fo);
+            if (live) fwd_qk<D, MQ, NKB, SEED>(sacc, st, Kc, fo);
             if (more) {
-                ks.load((j + 1) * KT);
-                vs.load((j + 1) * KT);
+                ks.load((j + 1) * KS * KT);
+                vs.load((j + 1) * KS * KT);
             }
-            const bool b = j == last_ragged ? fwd_softmax_pv_fast<D, MQ, true, NKB, SEED>(st, sacc, Vc, fo, j * KT, S, h)
-                                            : fwd_softmax_pv_fast<D, MQ, false, NKB, SEED>(st, sacc, Vc, fo, j * KT, S, h);
+            bool b = false;
+            if (live)
+                b = jj == last_ragged ? fwd_softmax_pv_fast<D, MQ, true, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h)
+                                      : fwd_softmax_pv_fast<D, MQ, false, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h);
             if (more) {
                 ks.store(Kn, 1.f, tid);
                 vs.store(Vn, 1.f, tid);
@@ -668,11 +674,13 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             __syncthreads();
             return b;
         };
-        step(smem, smem + TILE, smem + 2 * TILE, smem + 3 * TILE, 0, 1 < nsteps);
+        step(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, 0, 1 < nsteps);
         bool bad = false;
         for (int j = 1; j < nsteps; j += 2) {
-            bad = stepf(smem + 2 * TILE, smem + 3 * TILE, smem, smem + TILE, j, j + 1 < nsteps) || bad;
-            if (j + 1 < nsteps) bad = stepf(smem, smem + TILE, smem + 2 * TILE, smem + 3 * TILE, j + 1, j + 2 < nsteps) || bad;
+            bad = stepf(smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j, j + 1 < nsteps) || bad;
+            if (j + 1 < nsteps)
+                bad = stepf(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, j + 1, j + 2 < nsteps) ||
+                      bad;
         }
         if (__syncthreads_or(bad)) {
 #pragma unroll
@@ -686,7 +694,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             ks.load(0);
             vs.load(0);
             ks.store(smem, 1.f, tid);
-            vs.store(smem + TILE, 1.f, tid);
+            vs.store(smem + KS * TILE, 1.f, tid);
             __syncthreads();
             robust_loop();
         }
