@@ -471,6 +471,11 @@ __device__ __forceinline__ bool fwd_softmax_pv_fast(FwdState<D> (&st)[MQ], f32x1
     return bad;
 }
 
+template <int M>
+struct MaskTag {
+    static constexpr int value = M;
+};
+
 template <int D, bool SEED = true>
 __device__ __forceinline__ void fwd_init(FwdState<D>& st, const float* Q, long base, int q, int S, int h) {
     const float qscale = FA2_LOG2E / __builtin_sqrtf((float)D);
@@ -653,8 +658,12 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     // fwd + bwd step -1 .. -2 %.
     constexpr bool FWD_FAST = true;
     if constexpr (FWD_FAST) {
-        auto stepf = [&](const _Float16* Kc, const _Float16* Vc, _Float16* Kn, _Float16* Vn, int j, bool more)
-            __attribute__((always_inline)) {
+        // mt: MaskTag<0>: full tiles only (no masked copy of the tile body to join with,
+        // which left ~20 register copies per tile at D = 64); MaskTag<1>: the ragged
+        // last tile masked where it comes up
+        auto stepf = [&](auto mt, const _Float16* Kc, const _Float16* Vc, _Float16* Kn, _Float16* Vn, int j,
+                         bool more) __attribute__((always_inline)) {
+            constexpr bool RAG = decltype(mt)::value != 0;
             const int jj = j * KS + kg;                // this wave's tile
             const bool live = KS == 1 || jj < ntiles;  // wave-uniform (KS > 1: ragged tail)
             f32x16 sacc[MQ][NKB];
@@ -664,9 +673,13 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                 vs.load((j + 1) * KS * KT);
             }
             bool b = false;
-            if (live)
-                b = jj == last_ragged ? fwd_softmax_pv_fast<D, MQ, true, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h)
-                                      : fwd_softmax_pv_fast<D, MQ, false, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h);
+            if constexpr (RAG) {
+                if (live)
+                    b = jj == last_ragged ? fwd_softmax_pv_fast<D, MQ, true, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h)
+                                          : fwd_softmax_pv_fast<D, MQ, false, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h);
+            } else {
+                if (live) b = fwd_softmax_pv_fast<D, MQ, false, NKB, SEED>(st, sacc, Vc, fo, jj * KT, S, h);
+            }
             if (more) {
                 ks.store(Kn, 1.f, tid);
                 vs.store(Vn, 1.f, tid);
@@ -675,12 +688,25 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             return b;
         };
         step(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, 0, 1 < nsteps);
+        // D <= 64: the ragged last tile's step (always the last one) runs after the loop
+        // (r03 A/B: B2_H8 fwd S = 512 -7 %, S = 1024 -5 %, C3 -1.2 %); D = 128 keeps it
+        // in the loop (peeled, its 32-key-tile loop ran 5.8 % slower at C4)
+        constexpr bool PEEL = D <= 64;
+        using LoopTag = MaskTag<PEEL ? 0 : 1>;
+        const int jend = PEEL && last_ragged >= 0 && nsteps > 1 ? nsteps - 1 : nsteps;
         bool bad = false;
-        for (int j = 1; j < nsteps; j += 2) {
-            bad = stepf(smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j, j + 1 < nsteps) || bad;
-            if (j + 1 < nsteps)
-                bad = stepf(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, j + 1, j + 2 < nsteps) ||
+        for (int j = 1; j < jend; j += 2) {
+            bad = stepf(LoopTag{}, smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j,
+                        j + 1 < nsteps) ||
+                  bad;
+            if (j + 1 < jend)
+                bad = stepf(LoopTag{}, smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, j + 1,
+                            j + 2 < nsteps) ||
                       bad;
+        }
+        if (jend < nsteps) {  // j = nsteps - 1 >= 1: its buffers by parity (odd: the second pair)
+            _Float16* const kc = (jend & 1) ? smem + 2 * KS * TILE : smem;
+            bad = stepf(MaskTag<1>{}, kc, kc + KS * TILE, smem, smem, jend, false) || bad;
         }
         if (__syncthreads_or(bad)) {
 #pragma unroll
