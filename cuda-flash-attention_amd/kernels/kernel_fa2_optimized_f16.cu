@@ -665,7 +665,8 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
                          bool more) __attribute__((always_inline)) {
             constexpr bool RAG = decltype(mt)::value != 0;
             const int jj = j * KS + kg;                // this wave's tile
-            const bool live = KS == 1 || jj < ntiles;  // wave-uniform (KS > 1: ragged tail)
+            // wave-uniform (KS > 1: ragged tail); full steps (MaskTag<0>) have every group live
+            const bool live = KS == 1 || !RAG || jj < ntiles;
             f32x16 sacc[MQ][NKB];
             if (live) fwd_qk<D, MQ, NKB, SEED>(sacc, st, Kc, fo);
             if (more) {
@@ -693,7 +694,8 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         // in the loop (peeled, its 32-key-tile loop ran 5.8 % slower at C4)
         constexpr bool PEEL = D <= 64;
         using LoopTag = MaskTag<PEEL ? 0 : 1>;
-        const int jend = PEEL && last_ragged >= 0 && nsteps > 1 ? nsteps - 1 : nsteps;
+        // (KS > 1: also a last step where some key group has no tile)
+        const int jend = PEEL && (last_ragged >= 0 || ntiles % KS != 0) && nsteps > 1 ? nsteps - 1 : nsteps;
         bool bad = false;
         for (int j = 1; j < jend; j += 2) {
             bad = stepf(LoopTag{}, smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j,
