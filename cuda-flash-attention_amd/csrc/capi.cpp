@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -354,9 +355,22 @@ int run_shard(HostJob& j) {
     std::vector<int> h0(nch + 1);
     for (int c = 0; c <= nch; ++c) h0[c] = (int)((long)j.nheads * c / nch);
 
-    // D2H thread: waits for each chunk's kernels, copies its outputs back
-    std::atomic<int> issued{0};  // chunks whose kernels are enqueued
-    std::atomic<bool> abort{false};
+    // D2H thread: waits for each chunk's kernels, copies its outputs back.  It blocks
+    // on a condition variable until the chunk's kernels are enqueued (no spinning: with
+    // one such thread per shard, spinners would compete with the H2D threads for the
+    // host cores).
+    std::mutex issue_mu;
+    std::condition_variable issue_cv;
+    int issued = 0;  // chunks whose kernels are enqueued (guarded by issue_mu)
+    bool abort = false;
+    auto publish = [&](int n, bool ab) {
+        {
+            std::lock_guard<std::mutex> g(issue_mu);
+            if (n > issued) issued = n;
+            abort = abort || ab;
+        }
+        issue_cv.notify_one();
+    };
     int out_rc = FA2_OK;
     std::string out_err;
     std::thread d2h([&] {
@@ -366,9 +380,11 @@ int run_shard(HostJob& j) {
             return;
         }
         for (int c = 0; c < nch; ++c) {
-            while (issued.load(std::memory_order_acquire) <= c && !abort.load(std::memory_order_acquire))
-                std::this_thread::yield();
-            if (abort.load(std::memory_order_acquire)) return;
+            {
+                std::unique_lock<std::mutex> g(issue_mu);
+                issue_cv.wait(g, [&] { return issued > c || abort; });
+                if (abort) return;
+            }
             int e;
             if ((e = hip_status(hipStreamWaitEvent(r.so, r.ev[3 * c + 2], 0), "hipStreamWaitEvent"))) {
                 out_rc = e;
@@ -399,7 +415,7 @@ int run_shard(HostJob& j) {
         for (hipStream_t s : {r.si, r.sc, r.so}) (void)hipStreamSynchronize(s);
     };
     auto stop = [&](int code) {
-        abort.store(true, std::memory_order_release);
+        publish(0, true);
         d2h.join();
         drain();
         return code;
@@ -429,7 +445,7 @@ int run_shard(HostJob& j) {
                               r.sc);
         if (rc) return stop(rc);
         if ((rc = hip_status(hipEventRecord(r.ev[3 * c + 2], r.sc), "hipEventRecord"))) return stop(rc);
-        issued.store(c + 1, std::memory_order_release);
+        publish(c + 1, false);
     }
     d2h.join();
     if (out_rc) {

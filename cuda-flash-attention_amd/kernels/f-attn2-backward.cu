@@ -2,21 +2,34 @@
 //
 // Replaces detker/CUDA-Flash-Attention kernels/f-attn2-backward.cu
 // (flash_attention2_backward_kernel :33-339, D_computation_reduction_kernel
-// :341-380, host launcher :384-488, CuPy wrappers :491-528).  Same contract:
+// :341-380, host launcher :384-488, CuPy wrappers :491-528).  Same results:
 //   Δ_i = Σ_d dO_id·O_id                              (:341-380)
-//   per 32-key block: P = exp(QKᵀ/√D − LSE), dV += PᵀdO, dS = P∘(dOVᵀ − Δ)/√D,
-//   dQ += dS·K through global fp32 atomics (dQ pre-zeroed by the caller, :427-429,
-//   harness :546-548), dK += dSᵀQ; dK/dV written once (:326-338).
+//   P = exp(QKᵀ/√D − LSE), dV = PᵀdO, dS = P∘(dOVᵀ − Δ)/√D, dK = dSᵀQ, dQ = dS·K.
 //
-// Launch geometry = the reference harness's (test_flash_attention2.py:499-535):
-// backward grid B·H·⌈S/32⌉ x 256 threads (one workgroup per 32 keys), Δ kernel
-// B·H·S x 64 threads.  The four waves of a workgroup split the query range (wave
-// w takes every 4th 32-row query tile of a 128-row super-tile staged in LDS) and
-// sum their dKᵀ/dVᵀ register accumulators through LDS at the end.  All five
-// products run on v_mfma_f32_32x32x2_f32 (exact fp32): S and dP with the key on
-// the lane so the P / dS accumulator registers feed dVᵀ += dOᵀP and dKᵀ += QᵀdS
-// directly as B operands; dS crosses LDS once, for dQ = dS·K, whose 32x32
-// accumulator is added to HBM with row-segment-shaped global_atomic_add_f32.
+// The reference adds dQ into a pre-zeroed buffer with global fp32 atomics from every
+// 32-key workgroup (:269-301, zeroing at :427-429 / harness :546-548).  Here dQ has
+// no atomics and needs no pre-zeroing: a workgroup in the dQ ROLE owns 32 query
+// rows and walks all keys (recomputing S and dP for them), so every dQ element is
+// summed in one fixed order inside one workgroup and written once.  Results are
+// bitwise reproducible and no cross-XCD read-modify-write of dQ exists (r03's
+// zero-then-atomics design lost one key block's dQ on a driver box: the per-XCD L2s
+// are not coherent with each other, MI355X_MICROARCH §XCD placement).
+//
+// Roles (both on v_mfma_f32_32x32x2_f32, exact fp32 products, fp32 accumulation):
+//   dK/dV role (4 GEMMs): 32 keys per workgroup; the four waves split the query
+//     range (wave w takes every 4th 32-row tile of a 128-row Q/dO super-tile staged
+//     in LDS) and sum their dKᵀ/dVᵀ register accumulators through LDS at the end.
+//     S and dP have the key on the lane, so the P / dS accumulator registers feed
+//     dVᵀ += dOᵀP and dKᵀ += QᵀdS directly as B operands.
+//   dQ role (3 GEMMs): 32 queries per workgroup; the four waves split the key range
+//     (wave w takes every 4th 32-key tile of a 128-key K/V super-tile) and sum their
+//     dQᵀ accumulators through LDS.  Sᵀ and dPᵀ have the QUERY on the lane, so the
+//     −LSE / −Δ seeds are one lane constant each and the dSᵀ accumulator registers
+//     feed dQᵀ += KᵀdSᵀ directly as B operands.
+// The library launch (launch_backward_f32) runs the two roles side by side in one
+// grid of 2·B·H·⌈S/32⌉ workgroups after the Δ kernel.  The CuPy face keeps the
+// harness's grid B·H·⌈S/32⌉ x 256 threads (test_flash_attention2.py:499-535): each
+// workgroup runs the dK/dV role for key block i, then the dQ role for query block i.
 //
 // Self-contained device code (hiprtc -std=c++14 -DCUPY_INLINE_COMPILE).
 #ifndef CUPY_INLINE_COMPILE
@@ -98,49 +111,45 @@ __device__ __forceinline__ void delta_row_body(const float* __restrict__ dO, con
 }
 
 // Library Δ kernel: D/4 lanes per row (float4 loads), grid-stride over rows.
-// zero != nullptr: also clears those rows of `zero` (the fp32 backward's dQ, which its
-// kernel then accumulates with atomics): one launch instead of a memset and Δ.
 template <int D>
 __global__ void __launch_bounds__(256) fa2_delta_kernel(const float* __restrict__ dO, const float* __restrict__ O,
-                                                        float* __restrict__ Dvec, long rows,
-                                                        float* __restrict__ zero = nullptr) {
+                                                        float* __restrict__ Dvec, long rows) {
     constexpr int LPR = D / 4;  // lanes per row
     const long stride = (long)gridDim.x * (256 / LPR);
     const int sub = threadIdx.x % LPR;
-    for (long row = (long)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; row < rows + 0; row += stride) {
+    for (long row = (long)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; row < rows; row += stride) {
         const f32x4 a = *reinterpret_cast<const f32x4*>(dO + row * D + 4 * sub);
         const f32x4 b = *reinterpret_cast<const f32x4*>(O + row * D + 4 * sub);
         float acc = a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
 #pragma unroll
         for (int off = LPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
         if (sub == 0) Dvec[row] = acc;
-        if (zero) *reinterpret_cast<f32x4*>(zero + row * D + 4 * sub) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 }
 
 // ---------------------------------------------------------------------------
-// backward body: 32 keys per workgroup of 4 waves, grid = BH * ceil(S/32)
+// LDS of both roles, in two regions:
+//   TR = a 128-row super-tile (Q/dO for dK/dV, K/V for dQ; the 4-wave merge buffer
+//        of either role at the end) + the dK/dV role's lse2 / Δ rows;
+//   KD = two 32-row tiles (this block's K and V for dK/dV, its Q and dO for dQ).
 // ---------------------------------------------------------------------------
-// LDS of the backward body in two regions: TR = the Q/dO super-tile (also the
-// dK/dV merge buffer) + the super-tile's lse2/delta rows; KD = this workgroup's
-// K and V tiles + the per-wave dS transpose scratch.
 template <int D> struct BwdLds {
     static constexpr int LD = D + 4;
     static constexpr int T = 128 * LD;
     static constexpr int ROWS = 2 * 128;
     static constexpr int KV = 32 * LD;
-    static constexpr int DS = 4 * 32 * 33;
     static constexpr int TR = T + ROWS;
-    static constexpr int KD = 2 * KV + DS;
+    static constexpr int KD = 2 * KV;
     static constexpr int FLOATS = TR + KD;
 };
 
+// dK/dV role: key block `blk` (bh = blk / ⌈S/32⌉), 32 keys, 4 waves over the queries.
 template <int D>
-__device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const float* __restrict__ K,
-                                             const float* __restrict__ V, const float* __restrict__ dO,
-                                             const float* __restrict__ LSE, const float* __restrict__ Delta,
-                                             float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV,
-                                             int BH, int S, float* tr_lds, float* kd_lds) {
+__device__ __forceinline__ void dkdv_f32_body(const float* __restrict__ Q, const float* __restrict__ K,
+                                              const float* __restrict__ V, const float* __restrict__ dO,
+                                              const float* __restrict__ LSE, const float* __restrict__ Delta,
+                                              float* __restrict__ dK, float* __restrict__ dV, int BH, int S, int blk,
+                                              float* tr_lds, float* kd_lds) {
     constexpr int LD = D + 4;
     constexpr int QS = 128;
     float* T = tr_lds;
@@ -148,18 +157,16 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
     float* del = lse2 + QS;
     float* Kt = kd_lds;
     float* Vt = Kt + BwdLds<D>::KV;
-    float* Ds = Vt + BwdLds<D>::KV;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
     const int nkb = (S + 31) / 32;
-    const int bh = blockIdx.x / nkb, kb = blockIdx.x - bh * nkb;
+    const int bh = blk / nkb, kb = blk - bh * nkb;
     if (bh >= BH) return;
     const long base = (long)bh * S * D;
     const long rbase = (long)bh * S;
     const int k0 = kb * 32;
     const float qscale = FA2FB_LOG2E / __builtin_sqrtf((float)D);
     const float dscale = 1.f / __builtin_sqrtf((float)D);
-    float* Dsw = Ds + wave * 32 * 33;
 
     stage_rows<D>(Kt, K + base, k0, 32, S, tid, 1.f);
     stage_rows<D>(Vt, V + base, k0, 32, S, tid, 1.f);
@@ -175,7 +182,7 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
 
     // Q and dO super-tiles go HBM -> registers one compute phase before they are
     // needed (RowStage), so each LDS restage costs a barrier pair but no round trip:
-    // dO(st) loads during S(st), Q(st + 1) loads during dK / dQ(st).  Q(st) is loaded
+    // dO(st) loads during S(st), Q(st + 1) loads during dK(st).  Q(st) is loaded
     // once and stored twice from the same registers: scaled for S, unscaled for dK.
     const int nsuper = (S + QS - 1) / QS;
     RowStage<D, QS> rq, rd;
@@ -239,9 +246,6 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
             for (int b = 0; b < D / 32; ++b)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) dva[b] = mfma(Tw[acc_row(i, h) * LD + 32 * b + r], p[i], dva[b]);
-            // dS -> per-wave scratch [q][key] for dQ
-#pragma unroll
-            for (int i = 0; i < 16; ++i) Dsw[acc_row(i, h) * 33 + r] = ds[i];
         }
         // ---- Q (unscaled, from the same registers) for dK; the next super-tile's row
         // constants (lse2 / del are read only by the S and dP phases, both done)
@@ -259,21 +263,6 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
             for (int b = 0; b < D / 32; ++b)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) dka[b] = mfma(Tw[acc_row(i, h) * LD + 32 * b + r], ds[i], dka[b]);
-            // dQ[q][d] += dS[q][:] K[:][d] / sqrt(D), one 32x32 block per 32 columns
-#pragma unroll
-            for (int b = 0; b < D / 32; ++b) {
-                f32x16 acc;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-                for (int s = 0; s < 16; ++s)
-                    acc = mfma(Dsw[r * 33 + 2 * s + h], Kt[(2 * s + h) * LD + 32 * b + r], acc);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int qi = qw + acc_row(i, h);
-                    if (qi < S) atomicAdd(dQ + base + (long)qi * D + 32 * b + r, acc[i] * dscale);
-                }
-            }
         }
         // ---- the next super-tile's Q, scaled
         if (more) {
@@ -309,13 +298,145 @@ __device__ __forceinline__ void bwd_f32_body(const float* __restrict__ Q, const 
     }
 }
 
+// dQ role: query block `blk` (bh = blk / ⌈S/32⌉), 32 queries, 4 waves over the keys.
+// Per 128-key super-tile, one LDS buffer holds V (for dPᵀ) and then K (for Sᵀ and
+// dQᵀ): dPᵀ (16 registers) is kept across the restage, so K and V never need LDS
+// at the same time.  One RowStage carries K(st) during dPᵀ(st) and V(st + 1)
+// during Sᵀ/dQᵀ(st).
+template <int D>
+__device__ __forceinline__ void dq_f32_body(const float* __restrict__ Q, const float* __restrict__ K,
+                                            const float* __restrict__ V, const float* __restrict__ dO,
+                                            const float* __restrict__ LSE, const float* __restrict__ Delta,
+                                            float* __restrict__ dQ, int BH, int S, int blk, float* t_lds,
+                                            float* qd_lds) {
+    constexpr int LD = D + 4;
+    constexpr int KS = 128;
+    float* T = t_lds;
+    float* Qt = qd_lds;
+    float* Dt = qd_lds + 32 * LD;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    const int nqb = (S + 31) / 32;
+    const int bh = blk / nqb, qb = blk - bh * nqb;
+    if (bh >= BH) return;
+    const long base = (long)bh * S * D;
+    const long rbase = (long)bh * S;
+    const int q0 = qb * 32;
+    const float qscale = FA2FB_LOG2E / __builtin_sqrtf((float)D);
+    const float dscale = 1.f / __builtin_sqrtf((float)D);
+
+    stage_rows<D>(Qt, Q + base, q0, 32, S, tid, qscale);
+    stage_rows<D>(Dt, dO + base, q0, 32, S, tid, 1.f);
+    // this lane's query (column of every accumulator): the −LSE·log2e and −Δ seeds
+    const int qi = q0 + r;
+    const float nlse = qi < S ? -LSE[rbase + qi] * FA2FB_LOG2E : -__builtin_inff();
+    const float ndel = qi < S ? -Delta[rbase + qi] : 0.f;
+
+    f32x16 dqa[D / 32];
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dqa[b][i] = 0.f;
+
+    const int nsuper = (S + KS - 1) / KS;
+    RowStage<D, KS> rs;
+    rs.load(V + base, 0, S, tid);
+    rs.store(T, 1.f, tid);
+    __syncthreads();
+    rs.load(K + base, 0, S, tid);
+    for (int st = 0; st < nsuper; ++st) {
+        const int k0 = st * KS;
+        const int kw = k0 + 32 * wave;  // this wave's 32 keys
+        const bool active = kw < S;
+        const bool more = st + 1 < nsuper;
+        const float* Tw = T + 32 * wave * LD;
+        // ---- dPᵀ = V dOᵀ − Δ: keys on the registers' rows, queries on the lanes
+        f32x16 dp;
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dp[i] = ndel;
+#pragma unroll
+            for (int m = 0; m < D / 8; ++m) {
+                const f32x4 a = *reinterpret_cast<const f32x4*>(Tw + r * LD + 8 * m + 4 * h);
+                const f32x4 b = *reinterpret_cast<const f32x4*>(Dt + r * LD + 8 * m + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dp = mfma(a[e], b[e], dp);
+            }
+        }
+        // ---- K over V
+        __syncthreads();
+        rs.store(T, 1.f, tid);
+        __syncthreads();
+        if (more) rs.load(V + base, k0 + KS, S, tid);
+        if (active) {
+            // Sᵀ = K (Q·log2e/√D)ᵀ − LSE·log2e, Pᵀ = exp2, dSᵀ = Pᵀ ∘ dPᵀ
+            f32x16 p;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) p[i] = nlse;
+#pragma unroll
+            for (int m = 0; m < D / 8; ++m) {
+                const f32x4 a = *reinterpret_cast<const f32x4*>(Tw + r * LD + 8 * m + 4 * h);
+                const f32x4 b = *reinterpret_cast<const f32x4*>(Qt + r * LD + 8 * m + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) p = mfma(a[e], b[e], p);
+            }
+            f32x16 ds;
+            if (kw + 32 <= S) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) ds[i] = fast_exp2(p[i]) * dp[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) ds[i] = kw + acc_row(i, h) < S ? fast_exp2(p[i]) * dp[i] : 0.f;
+            }
+            // dQᵀ += Kᵀ dSᵀ: step i takes accumulator register i as B (k = h <-> key acc_row(i, h))
+#pragma unroll
+            for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dqa[b] = mfma(Tw[acc_row(i, h) * LD + 32 * b + r], ds[i], dqa[b]);
+        }
+        // ---- the next super-tile's V
+        if (more) {
+            __syncthreads();
+            rs.store(T, 1.f, tid);
+            __syncthreads();
+            rs.load(K + base, k0 + KS, S, tid);
+        }
+    }
+
+    // ---- sum the four waves' dQᵀ through LDS and write rows [q0, q0+32)
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 v = {dqa[b][4 * g], dqa[b][4 * g + 1], dqa[b][4 * g + 2], dqa[b][4 * g + 3]};
+            *reinterpret_cast<f32x4*>(T + (wave * 32 + r) * LD + 32 * b + 8 * g + 4 * h) = v;
+        }
+    __syncthreads();
+    for (int x = tid; x < 32 * (D / 4); x += 256) {
+        const int row = x / (D / 4), c4 = x - row * (D / 4);
+        if (q0 + row < S) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int w = 0; w < 4; ++w) acc += *reinterpret_cast<const f32x4*>(T + (w * 32 + row) * LD + 4 * c4);
+            *reinterpret_cast<f32x4*>(dQ + base + (long)(q0 + row) * D + 4 * c4) = acc * dscale;
+        }
+    }
+}
+
+// One launch, two roles: workgroups [0, nblk) take the dK/dV role for key block
+// blockIdx.x, workgroups [nblk, 2·nblk) the dQ role for query block blockIdx.x − nblk.
 template <int D>
 __global__ void __launch_bounds__(256)
 fa2_bwd_f32_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                    const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-                   float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV, int BH, int S) {
+                   float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV, int BH, int S, int nblk) {
     __shared__ __attribute__((aligned(16))) float smem[BwdLds<D>::FLOATS];
-    bwd_f32_body<D>(Q, K, V, dO, LSE, Delta, dQ, dK, dV, BH, S, smem, smem + BwdLds<D>::TR);
+    const int blk = blockIdx.x;
+    if (blk < nblk)
+        dkdv_f32_body<D>(Q, K, V, dO, LSE, Delta, dK, dV, BH, S, blk, smem, smem + BwdLds<D>::TR);
+    else
+        dq_f32_body<D>(Q, K, V, dO, LSE, Delta, dQ, BH, S, blk - nblk, smem, smem + BwdLds<D>::TR);
 }
 
 }  // namespace fa2f32b
@@ -325,23 +446,22 @@ namespace fa2 {
 
 namespace {
 template <int D>
-hipError_t delta_dispatch(const float* dout, const float* o, float* delta, int bh, int S, hipStream_t stream,
-                          float* zero = nullptr) {
+hipError_t delta_dispatch(const float* dout, const float* o, float* delta, int bh, int S, hipStream_t stream) {
     const long rows = (long)bh * S;
     const long rows_per_block = 256 / (D / 4);
     long grid = (rows + rows_per_block - 1) / rows_per_block;
     if (grid > 8192) grid = 8192;
     hipLaunchKernelGGL((fa2f32b::fa2_delta_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, dout, o, delta,
-                       rows, zero);
+                       rows);
     return hipGetLastError();
 }
 template <int D>
 hipError_t bwd_f32_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                             const float* delta, float* dq, float* dk, float* dv, int bh, int S, hipStream_t stream) {
-    const long grid = (long)bh * ((S + 31) / 32);
-    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f32b::fa2_bwd_f32_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, dout,
-                       lse, delta, dq, dk, dv, bh, S);
+    const long nblk = (long)bh * ((S + 31) / 32);
+    if (nblk <= 0 || 2 * nblk > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f32b::fa2_bwd_f32_kernel<D>), dim3((unsigned)(2 * nblk)), dim3(256), 0, stream, q, k, v,
+                       dout, lse, delta, dq, dk, dv, bh, S, (int)nblk);
     return hipGetLastError();
 }
 }  // namespace
@@ -360,13 +480,7 @@ hipError_t launch_backward_f32(int D, const float* q, const float* k, const floa
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream) {
     if (bh <= 0 || S <= 0 || !supported_head_dim(D)) return hipErrorInvalidValue;
-    // Δ, with dQ cleared in the same pass (the kernel below adds into it)
-    hipError_t e;
-    switch (D) {
-        case 32: e = delta_dispatch<32>(dout, o, delta, bh, S, stream, dq); break;
-        case 64: e = delta_dispatch<64>(dout, o, delta, bh, S, stream, dq); break;
-        default: e = delta_dispatch<128>(dout, o, delta, bh, S, stream, dq); break;
-    }
+    const hipError_t e = launch_delta(D, dout, o, delta, bh, S, stream);
     if (e != hipSuccess) return e;
     switch (D) {
         case 32: return bwd_f32_dispatch<32>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
@@ -407,12 +521,14 @@ FA2_INST_BWD32(32)
 FA2_INST_BWD32(64)
 FA2_INST_BWD32(128)
 #else
-// CuPy face (test_flash_attention2.py:132-141, 499-535).  dQ/dK/dV arrive zeroed.
+// CuPy face (test_flash_attention2.py:132-141, 499-535).  The harness hands dQ/dK/dV
+// in zeroed; here every element is overwritten.  Grid B·H·⌈S/32⌉: workgroup i runs
+// the dK/dV role for key block i, then the dQ role for query block i.
 // LDS: the launch adds the harness's dynamic bytes ((32D + 4*32D + 32 + 32*32)*4,
 // 45 184 at D=64, :522-527) to this kernel's static bytes, and the sum must stay
 // within the 160 KiB a workgroup may own.  Static LDS is therefore sized for
-// D <= 64 (70 KB); at D = 128 the Q/dO super-tile moves into the dynamic region
-// (86 KB provided there).  The dispatch packet's group_segment_size (static +
+// D <= 64 (53 KB); at D = 128 the 128-row super-tile region moves into the dynamic
+// region (86 KB provided there).  The dispatch packet's group_segment_size (static +
 // dynamic) is checked first, so an undersized launch writes nothing instead of
 // running past its LDS.
 __device__ __forceinline__ unsigned fa2_group_segment_bytes() {
@@ -430,18 +546,27 @@ flash_attention2_backward_kernel_wrapper(const float* query, const float* key, c
     extern __shared__ __attribute__((aligned(16))) float dyn[];
     (void)output;
     const int bh = batch_size * num_heads;
+    const int blk = blockIdx.x;
     const unsigned have = fa2_group_segment_bytes();
     if (head_dim == 64) {
-        fa2f32b::bwd_f32_body<64>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
-                                  smem, smem + fa2f32b::BwdLds<64>::TR);
+        float* kd = smem + fa2f32b::BwdLds<64>::TR;
+        fa2f32b::dkdv_f32_body<64>(query, key, value, d_output, logsumexp, d, d_key, d_value, bh, seq_len, blk, smem,
+                                   kd);
+        __syncthreads();
+        fa2f32b::dq_f32_body<64>(query, key, value, d_output, logsumexp, d, d_query, bh, seq_len, blk, smem, kd);
     } else if (head_dim == 32) {
-        fa2f32b::bwd_f32_body<32>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
-                                  smem, smem + fa2f32b::BwdLds<32>::TR);
+        float* kd = smem + fa2f32b::BwdLds<32>::TR;
+        fa2f32b::dkdv_f32_body<32>(query, key, value, d_output, logsumexp, d, d_key, d_value, bh, seq_len, blk, smem,
+                                   kd);
+        __syncthreads();
+        fa2f32b::dq_f32_body<32>(query, key, value, d_output, logsumexp, d, d_query, bh, seq_len, blk, smem, kd);
     } else if (head_dim == 128) {
         if (have < sizeof(smem) + 4u * fa2f32b::BwdLds<128>::TR) return;
         static_assert(fa2f32b::BwdLds<128>::KD <= fa2f32b::BwdLds<64>::FLOATS, "KD region must fit the static LDS");
-        fa2f32b::bwd_f32_body<128>(query, key, value, d_output, logsumexp, d, d_query, d_key, d_value, bh, seq_len,
-                                   dyn, smem);
+        fa2f32b::dkdv_f32_body<128>(query, key, value, d_output, logsumexp, d, d_key, d_value, bh, seq_len, blk, dyn,
+                                    smem);
+        __syncthreads();
+        fa2f32b::dq_f32_body<128>(query, key, value, d_output, logsumexp, d, d_query, bh, seq_len, blk, dyn, smem);
     }
 }
 

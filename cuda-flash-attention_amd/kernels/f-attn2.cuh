@@ -77,8 +77,9 @@ hipError_t launch_delta(int D, const float* dout, const float* o, float* delta, 
 hipError_t launch_backward_f16(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream);
-// exact-fp32 backward; dq is zeroed here (by the Δ kernel, on `stream`) and then
-// accumulated with global fp32 atomics, as f-attn2-backward.cu:298 does.
+// exact-fp32 backward: the Δ kernel, then one launch whose workgroups take the dK/dV
+// role (32 keys each) or the dQ role (32 queries each, S and dP recomputed); no float
+// atomics (the reference's dQ atomicAdd, f-attn2-backward.cu:298), bitwise reproducible.
 hipError_t launch_backward_f32(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream);

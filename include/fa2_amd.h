@@ -53,10 +53,9 @@ int fa2_delta(const float* dout, const float* o, float* delta, int batch, int he
               void* stream);
 
 /* Backward: dQ, dK, dV (fully overwritten; no pre-zeroing needed).  `delta` is
- * [B,H,S] scratch that receives Δ.  Determinism: FA2_FP16 / FA2_BF16 results are
- * bitwise reproducible (no float atomics in any launch plan).  FA2_FP32 adds dQ with
- * fp32 global atomics, as the reference does (f-attn2-backward.cu:298), so its dQ
- * may differ in the last bits between calls; its dK and dV are reproducible.
+ * [B,H,S] scratch that receives Δ.  Determinism: results are bitwise reproducible in
+ * every precision (no float atomics in any launch plan; the reference adds dQ with
+ * fp32 atomics, f-attn2-backward.cu:298, here a dQ workgroup role sums it instead).
  * Replaces the device half of host_flash_attention2_backward[_fp16] (kernels/f-attn2.cuh:26-41 / :56-71) and
  * the CuPy launches of D_computation_reduction_kernel_wrapper +
  * flash_attention2_backward_kernel_wrapper (f-attn2-backward.cu:491-528). */

@@ -5,6 +5,7 @@ C3 and C5 on this box's GPUs, for several head-chunk counts (HOST_CHUNKS); with
 import argparse
 import json
 import os
+import resource
 import statistics
 import sys
 import time
@@ -23,31 +24,42 @@ def timed(fa2amd, shape, ndev, runs):
     do = np.ones_like(q)
     o, lse = np.empty_like(q), np.empty((B, H, S), np.float32)
     dq, dk, dv = np.empty_like(q), np.empty_like(q), np.empty_like(q)
-    tf, tb = [], []
+    tf, tb, cpu = [], [], []
+    cpu_s = lambda: (lambda r: r.ru_utime + r.ru_stime)(resource.getrusage(resource.RUSAGE_SELF))
     for i in range(runs + 1):
+        c0 = cpu_s()
         t0 = time.perf_counter()
         fa2amd.forward_host(q, k, v, "fp16", num_devices=ndev, out=o, lse=lse)
         t1 = time.perf_counter()
         fa2amd.backward_host(q, k, v, o, do, lse, "fp16", num_devices=ndev, dq=dq, dk=dk, dv=dv)
         t2 = time.perf_counter()
+        c1 = cpu_s()
         if i:
             tf.append(t1 - t0)
             tb.append(t2 - t1)
+            cpu.append(c1 - c0)
     fb = 4 * B * H * S * (4 * D + 1)
     bb = 4 * B * H * S * (8 * D + 1)
     f, b = statistics.median(tf), statistics.median(tb)
     return {"fwd_ms": round(f * 1e3, 2), "fwd_gbps": round(fb / f / 1e9, 1), "bwd_ms": round(b * 1e3, 2),
-            "bwd_gbps": round(bb / b / 1e9, 1)}
+            "bwd_gbps": round(bb / b / 1e9, 1),
+            # host CPU seconds (user + system, all threads, getrusage) per fwd + bwd pair
+            "cpu_ms_per_pair": round(statistics.median(cpu) * 1e3, 2),
+            "cpu_over_wall": round(statistics.median(cpu) / (f + b), 2)}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shards-on-device0", type=int, default=0)
+    ap.add_argument("--lib", default=None, help="library build to load instead of the in-tree one")
+    ap.add_argument("--c5-only", action="store_true")
     args = ap.parse_args()
     import fa2amd
+    if args.lib:
+        fa2amd.use_library(args.lib)
 
     out = {}
-    for ch in (1, 2, 4, 0):
+    for ch in () if args.c5_only else (1, 2, 4, 0):
         fa2amd.tune_set("HOST_CHUNKS", ch)
         out[f"c3_chunks{ch or 'auto'}"] = timed(fa2amd, (4, 16, 2048, 64), 1, 4)
     fa2amd.tune_set(None)
