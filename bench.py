@@ -290,7 +290,11 @@ def extras(fa2amd, torch, dev):
                                             "frac_mfma_f32": round(tf / MFMA_F32_PEAK_TFLOPS, 4)}
     ms, tf, gbps = time_config(fa2amd, torch, dev, 64, 16, 2048, 64, "fp16", False, iters=10)
     out["c5_1gpu_B64_H16_S2048_D64_fp16_fwdbwd"] = roof_entry(ms, tf, gbps, 2048, False)
-    out["c3_host_api_pcie_inclusive"] = host_api_entry(fa2amd, 4, 16, 2048, 64)
+    try:
+        out["c3_host_api_pcie_inclusive"] = host_api_entry(fa2amd, 4, 16, 2048, 64)
+    except Exception as e:  # reported, never required
+        log("c3 host-API entry failed:", e)
+        out["c3_host_api_pcie_inclusive"] = None
     return out
 
 
@@ -523,7 +527,15 @@ def main():
         dist.barrier()
         if rank == 0 and not rehearse:
             Bc, Hc, Sc, Dc, _ = WORKLOADS["c5"]
-            extra["c5_host_api_pcie_inclusive"] = host_api_entry(fa2amd, Bc, Hc, Sc, Dc, runs=2, num_devices=world)
+            # reported, never required: a failure (fewer visible devices, memory beside the
+            # other ranks' buffers) is logged and recorded as null, and rank 0 still reaches
+            # the barrier the other ranks wait at
+            try:
+                extra["c5_host_api_pcie_inclusive"] = host_api_entry(fa2amd, Bc, Hc, Sc, Dc, runs=2,
+                                                                     num_devices=world)
+            except Exception as e:
+                log("c5 host-API entry failed:", e)
+                extra["c5_host_api_pcie_inclusive"] = None
         dist.barrier()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -924,6 +924,59 @@ __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, 
         }
 }
 
+// compile-time constants passed to generic lambdas (hiprtc has no <type_traits>)
+template <int V> struct CInt { static constexpr int value = V; };
+template <bool V> struct CBool { static constexpr bool value = V; };
+
+// The two halves of dq_tile16, for the pipelined loop (PIPE below): Sᵀ / dPᵀ of one
+// 32-key half kb and its dSᵀ (packed B operands), and that half's dQᵀ product.
+template <int D, bool MASK>
+__device__ __forceinline__ void dq_sdp16(const DqState16<D>& st, const _Float16* Ks, const _Float16* Vs,
+                                         const FragOffsets16<D>& fo, int k0, int S, int g, int kb, f16x8 (&dsf)[2]) {
+    f32x4 sa[2][2], da[2][2];  // [mbl][nb]: keys k0 + 32 kb + 16 mbl + 4g + i
+#pragma unroll
+    for (int mbl = 0; mbl < 2; ++mbl)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            sa[mbl][nb] = st.nlse2[nb];
+            da[mbl][nb] = st.ndel[nb];
+        }
+#pragma unroll
+    for (int ks = 0; ks < D / 32; ++ks)
+#pragma unroll
+        for (int mbl = 0; mbl < 2; ++mbl) {
+            const f16x8 ka = fo.rowop(Ks, 32 * kb + 16 * mbl, ks), va = fo.rowop(Vs, 32 * kb + 16 * mbl, ks);
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                sa[mbl][nb] = mfma16(ka, st.qf[nb][ks], sa[mbl][nb]);
+                da[mbl][nb] = mfma16(va, st.df[nb][ks], da[mbl][nb]);
+            }
+        }
+    if (MASK) {
+#pragma unroll
+        for (int mbl = 0; mbl < 2; ++mbl)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (k0 + 32 * kb + 16 * mbl + 4 * g + i >= S) sa[mbl][nb][i] = -__builtin_inff();
+    }
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsf[nb][j] = to_tile(fast_exp2(sa[j >> 2][nb][j & 3]) * da[j >> 2][nb][j & 3]);
+}
+template <int D>
+__device__ __forceinline__ void dq_prod16(DqState16<D>& st, const _Float16* Ks, const FragOffsets16<D>& fo, int kb,
+                                          const f16x8 (&dsf)[2]) {
+#pragma unroll
+    for (int md = 0; md < D / 16; ++md) {
+        const f16x8 a = fo.trop(Ks, 32 * kb, md);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) st.dqa[md][nb] = mfma16(a, dsf[nb], st.dqa[md][nb]);
+    }
+}
+
 // DELTA: Δ is computed here (from O, fused into the dO prologue) and written to
 // `Delta` for the dK/dV kernel, which then runs after this one.
 // NKB 32-key blocks per K/V tile (1 for D = 128 at 8 waves: fewer registers).
@@ -933,9 +986,10 @@ __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, 
 // summed in LDS in group order (deterministic) and group 0 stores.
 // The workgroup's LDS: [buf][K | V][KS] tiles (at least one Q block for the coalesced
 // prologue, and the key-split merge records), the per-wave dQ stage, the block's Δ.
-template <int D, int NW, bool DELTA, int NKB, int KS>
+template <int D, int NW, bool DELTA, int NKB, int KS, bool PIPE = false>
 struct DqLds {
     static constexpr int KT = 32 * NKB, TILE = KT * D, NQ = NW / KS;
+    // PIPE: K and V tiles in 3-slot rings (tile t in slot t % 3) instead of 2 buffers
     // key-split merge records: per wave of groups 1..KS-1, dQᵀ (D / 2 floats per lane)
     static constexpr int MERGE = KS > 1 ? 2 * (KS - 1) * NQ * (D / 2) * 64 : 0;  // in halves
     // OVL: the prologue's Q and dO blocks behind the first K/V buffer, loaded together
@@ -943,7 +997,8 @@ struct DqLds {
     // trips are exposed; on the unsplit C3 grid it measured -1.7 %)
     static constexpr bool OVL = KS > 1 || D == 128;
     static constexpr int QD = OVL ? 2 * KS * TILE + 2 * 32 * NQ * D : 32 * NQ * D;
-    static constexpr int SMEM0 = 4 * KS * TILE > QD ? 4 * KS * TILE : QD;
+    static constexpr int RING = PIPE ? 6 * TILE : 4 * KS * TILE;
+    static constexpr int SMEM0 = RING > QD ? RING : QD;
     static constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;  // halves
     static constexpr int OSTAGE = 2 * SMEM;                     // byte offsets
     static constexpr int DBLK = OSTAGE + NQ * 32 * 36 * 4;
@@ -952,13 +1007,25 @@ struct DqLds {
 
 // One workgroup of the dQ kernel; `bid` is its (XCD-remapped) block number over the
 // BH * ceil(S / (32 * NQ)) query blocks.
-template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1, int IGLP = -1>
+// PIPE (unsplit 16x16x32 instances, 64-key tiles): software-pipelined tile loop.  The
+// dQᵀ product of each tile's second 32-key half runs at the start of the NEXT step,
+// beside that step's Sᵀ / dPᵀ MFMAs, and the first half's product after the second
+// half's Sᵀ / dPᵀ, so no step ends on the dependent chain exp -> cvt -> (transposed
+// K read) -> dQ MFMA that both waves of a SIMD reach together before the barrier.
+// The deferred product reads the previous tile's K, so K and V live in 3-slot rings
+// (tile t in slot t % 3: the store of tile t + 1 overwrites tile t - 2, which the
+// barrier ending step t - 1 has retired).  Same products in the same order per
+// accumulator as the unpipelined loop, so dQ is bitwise unchanged.
+template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1, int IGLP = -1,
+          bool PIPE = false>
 __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const float* __restrict__ Q,
                                         const float* __restrict__ K, const float* __restrict__ V,
                                         const float* __restrict__ dO, const float* __restrict__ LSE,
                                         float* __restrict__ Delta, float* __restrict__ dQ, int S,
                                         const float* __restrict__ O) {
-    using L = DqLds<D, NW, DELTA, NKB, KS>;
+    using L = DqLds<D, NW, DELTA, NKB, KS, PIPE>;
+    static_assert(!PIPE || (M16 && KS == 1 && NKB == 2 && !L::OVL), "pipelined loop: unsplit 16x16x32, 64-key tiles");
+    constexpr int V0 = PIPE ? 3 * L::TILE : KS * L::TILE;  // first V buffer / slot
     constexpr int KT = L::KT;
     constexpr int NT = 64 * NW;
     constexpr int TILE = L::TILE;
@@ -993,7 +1060,7 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     // branches around the loads left 34 v_mov_b64 of staging-register copies there (dQ
     // +11.8 % without).  At D <= 64 the runtime flag stays: with it gone the compiler
     // schedules the mid-tile loads differently and dQ ran 4.5 % slower at C3.
-    ks.on = vs.on = (SW == NW && D > 64) || __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
+    ks.on = vs.on = (SW == NW && (D > 64 || PIPE)) || __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
     const int ntiles = (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     const int nsteps = (ntiles + KS - 1) / KS;
@@ -1052,7 +1119,7 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
         if (DELTA) delta_rows<D, 32 * NQ, NT>(dst, ost, S, qb * 32 * NQ, delta_blk, Delta + (long)bh * S, tid);
         if constexpr (OVL) {
             ks.store(smem, 1.f, tid);
-            vs.store(smem + KS * TILE, 1.f, tid);
+            vs.store(smem + V0, 1.f, tid);
         }
         __syncthreads();
         if constexpr (OVL) read_q();
@@ -1092,12 +1159,62 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
         ks.load(0);
         vs.load(0);
         ks.store(smem, 1.f, tid);
-        vs.store(smem + KS * TILE, 1.f, tid);
+        vs.store(smem + V0, 1.f, tid);
     }
     __syncthreads();
     // the group's tile within each staged image: folded into the per-lane offsets
     if (KS > 1) fo16.shift(kg * TILE);
 
+    if constexpr (PIPE) {
+        // tiles [0, nfull) unmasked in the loop, a ragged last tile after it
+        const int nfull = S / KT;
+        f16x8 dprev[2];  // dSᵀ of the previous tile's second 32-key half
+        auto kslot = [&](int sl) { return smem + sl * TILE; };
+        auto vslot = [&](int sl) { return smem + V0 + sl * TILE; };
+        // one step on tile t in slot SL; FIRST: no previous tile; MASK: the ragged tile
+        auto pstep = [&](auto SLc, auto FIRSTc, auto MASKc, int t) {
+            constexpr int SL = decltype(SLc)::value, SN = (SL + 1) % 3, SP = (SL + 2) % 3;
+            constexpr bool FIRST = decltype(FIRSTc)::value, MASK = decltype(MASKc)::value;
+            if constexpr (!FIRST) dq_prod16<D>(st16, kslot(SP), fo16, 1, dprev);
+            f16x8 d0[2];
+            dq_sdp16<D, MASK>(st16, kslot(SL), vslot(SL), fo16, t * KT, S, g16, 0, d0);
+            // the next tile's loads (past the end: out of the buffer's range, zeros)
+            ks.load((t + 1) * KT);
+            vs.load((t + 1) * KT);
+            dq_sdp16<D, MASK>(st16, kslot(SL), vslot(SL), fo16, t * KT, S, g16, 1, dprev);
+            dq_prod16<D>(st16, kslot(SL), fo16, 0, d0);
+            // slot SN held tile t - 2 (retired by the barrier that ended step t - 1);
+            // the store after the last tile writes zeros nobody reads
+            ks.store(kslot(SN), 1.f, tid);
+            vs.store(vslot(SN), 1.f, tid);
+            __syncthreads();
+        };
+        using I0 = CInt<0>;
+        using I1 = CInt<1>;
+        using I2 = CInt<2>;
+        using BT = CBool<true>;
+        using BF = CBool<false>;
+        int t = 0;
+        if (nfull > 0) {
+            pstep(I0(), BT(), BF(), 0);
+            t = 1;
+            for (; t + 3 <= nfull; t += 3) {
+                pstep(I1(), BF(), BF(), t);
+                pstep(I2(), BF(), BF(), t + 1);
+                pstep(I0(), BF(), BF(), t + 2);
+            }
+            if (t < nfull) pstep(I1(), BF(), BF(), t++);
+            if (t < nfull) pstep(I2(), BF(), BF(), t++);
+        }
+        if (t < ntiles) {  // the ragged last tile, slot t % 3
+            const int sl = t % 3;
+            if (t == 0) pstep(I0(), BT(), BT(), 0);
+            else if (sl == 0) pstep(I0(), BF(), BT(), t);
+            else if (sl == 1) pstep(I1(), BF(), BT(), t);
+            else pstep(I2(), BF(), BT(), t);
+        }
+        dq_prod16<D>(st16, kslot((ntiles - 1) % 3), fo16, 1, dprev);  // the last tile's second half
+    } else
     for (int j = 0; j < nsteps; j += 2) {
         {
             const bool more = j + 1 < nsteps;
@@ -1189,14 +1306,14 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     }
 }
 
-template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1>
+template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1, bool PIPE = false>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                       const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
                       float* __restrict__ dQ, int S, const float* __restrict__ O) {
-    __shared__ __attribute__((aligned(16))) char lds[DqLds<D, NW, DELTA, NKB, KS>::BYTES];
-    dq_body<D, NW, DELTA, NKB, M16, KS, KS == 1 && D == 64 ? FA2_IGLP_DQ : -1>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K,
-                                                                              V, dO, LSE, Delta, dQ, S, O);
+    __shared__ __attribute__((aligned(16))) char lds[DqLds<D, NW, DELTA, NKB, KS, PIPE>::BYTES];
+    dq_body<D, NW, DELTA, NKB, M16, KS, KS == 1 && D == 64 ? FA2_IGLP_DQ : -1, PIPE>(
+        lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE, Delta, dQ, S, O);
 }
 
 // dK/dV and dQ in ONE launch (small grids).  Workgroups [0, ndk) take the dK/dV role
@@ -1459,16 +1576,16 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     if (nw == 2) return dkdv_launch<D, 2, false>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
-template <int D, int NW, int NKB = 2, bool M16 = false, int KS = 1>
+template <int D, int NW, int NKB = 2, bool M16 = false, int KS = 1, bool PIPE = false>
 hipError_t dq_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                      float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
     const long grid = (long)bh * ((S + 32 * (NW / KS) - 1) / (32 * (NW / KS)));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
     if (o)
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB, M16, KS>), dim3((unsigned)grid),
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB, M16, KS, PIPE>), dim3((unsigned)grid),
                            dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     else
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB, M16, KS>), dim3((unsigned)grid),
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB, M16, KS, PIPE>), dim3((unsigned)grid),
                            dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     return hipGetLastError();
 }
@@ -1502,6 +1619,9 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     }
     // 16x16x32 (+2.4 % at C3 over 32x32x16) but at 2 waves
     if constexpr (D <= 64) {
+        // DQ_PIPE: the software-pipelined tile loop (dq_body PIPE)
+        if (nw == 8 && tune_knob("DQ_PIPE", 0))
+            return dq_launch<D, 8, 2, true, 1, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
         if (nw == 8) return dq_launch<D, 8, 2, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
         if (nw == 2) return dq_launch<D, 2>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
     }
@@ -1588,7 +1708,14 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
         const int fks = tune_knob("BWD_FKS", a >= 4 ? 1 : 2);
         // waves per workgroup of both roles (8, or 4 for the split pairs)
         const int fnw = tune_knob("BWD_FNW", tiny ? 4 : 8);
-        if (fqs == 1 && fks == 1) return fused_launch<D, 8, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
+        // an override combination no instance serves is an error, never a silent
+        // fallback to the two-kernel plan (an A/B would otherwise time the default)
+        const bool forced = tune_knob("BWD_FQS", 0) || tune_knob("BWD_FKS", 0) || tune_knob("BWD_FNW", 0);
+        if (fnw != 4 && fnw != 8) return hipErrorInvalidValue;
+        if (fqs == 1 && fks == 1) {
+            if (fnw != 8) return hipErrorInvalidValue;  // the unsplit roles exist at 8 waves only
+            return fused_launch<D, 8, 1, 1, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
+        }
         if (fnw == 4) {
             if (fqs == 2 && fks == 2)
                 return fused_launch<D, 4, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
@@ -1597,7 +1724,7 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
         }
         if (fqs == 2 && fks == 2) return fused_launch<D, 8, 2, 2, 2>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
         if (fqs == 2 && fks == 4) return fused_launch<D, 8, 2, 4, 1>(q, k, v, dout, lse, delta, dq, dk, dv, bh, S, o, stream);
-        return hipErrorNotSupported;
+        return forced ? hipErrorInvalidValue : hipErrorNotSupported;
     }
 }
 }  // namespace
