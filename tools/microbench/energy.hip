@@ -152,7 +152,11 @@ __global__ void __launch_bounds__(512) kern(float* out, int iters, const f32x4* 
 template <int MODE>
 double run(float* d, int iters, double secs, int* launches, const f32x4* src, long nsrc) {
     hipLaunchKernelGGL((kern<MODE>), dim3(256), dim3(512), 0, 0, d, 16, src, nsrc);
-    (void)hipDeviceSynchronize();
+    const hipError_t e0 = hipGetLastError(), e1 = hipDeviceSynchronize();
+    if (e0 != hipSuccess || e1 != hipSuccess) {
+        fprintf(stderr, "mode %d: launch %s, sync %s\n", MODE, hipGetErrorString(e0), hipGetErrorString(e1));
+        exit(3);
+    }
     auto t0 = std::chrono::steady_clock::now();
     int n = 0;
     double el = 0;
