@@ -36,6 +36,10 @@
 #define FA2_TILE_LAUNCH(x) x##_f16
 #define FA2_TILE_HOST(x) x##_fp16
 #endif
+#ifndef FA2_SP_ABL
+#define FA2_SP_ABL 0  // ablation builds (tools/ab_sp_parts.sh): 1 = no dQ product, 2 = no part stores
+#endif
+
 namespace fa2f16b {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -577,7 +581,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
                                           float* __restrict__ dV, int S, const float* __restrict__ O = nullptr,
                                           void* __restrict__ part = nullptr, long part_stride = 0,
                                           float* __restrict__ delta_out = nullptr) {
-    static_assert(!SP || (M16 && QS == 1 && KB == 1 && NW == 8 && D == 64 && DEL), "single pass: C3 geometry");
+    static_assert(!SP || (M16 && QS == 1 && KB == 1 && NW == 8 && D == 64), "single pass: C3 geometry");
     using L = DkdvLds<D, NW, KB, QS, SP>;
     constexpr int QT = L::QT;  // query rows per step
     constexpr int NT = 64 * NW;
@@ -776,6 +780,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         // dsf[nb]: key 16 nb + (l & 15) of this wave, k-slot j <-> query 16 (j >> 2) + 4g + (j & 3)
         // of the 32-query half qb: two 4-query runs per key, one 8-byte write each
         return [=](int qb, const f16x8 (&dsf)[2]) {
+            if constexpr (FA2_SP_ABL == 1) return;
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) {
                 const bool ok = nb ? kok1 : kok0;
@@ -806,6 +811,7 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         }
     }
     auto dq_part = [&](const _Float16* img, int t) {
+        if constexpr (FA2_SP_ABL == 1) return;
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int c = 0; c < KPW * NK / 32; ++c) {
@@ -818,6 +824,10 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         }
         // C[d = 16 (2 pd + m) + 4g + i][query 64 t + 16 pq + (l & 15)]: 4 consecutive columns per lane
         const int qrow = t * QT + 16 * pq + (lane & 15);
+        if constexpr (FA2_SP_ABL == 2) {
+            asm volatile("" ::"v"(acc[0]), "v"(acc[1]));
+            return;
+        }
         // K image is K·log2e/√D; the part is dS·K/√D
         const float sc = 1.f / FA2B_LOG2E;
 #pragma unroll
@@ -941,15 +951,21 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
 
 // Single-pass backward (SP): dK, dV, Δ and the dQ parts of every 256-key block in one
 // launch (grid BH * ceil(S / 256), 8 waves); fa2_bwd_sp_reduce then sums the parts.
-template <int SP>
+// SPDEL: Δ computed per step from O staged beside dO (all waves stage); else Δ is read
+// from `Delta`, which a prior fa2_delta launch wrote (four waves stage, as in dK/dV)
+#ifndef FA2_SP_DEL
+#define FA2_SP_DEL 0
+#endif
+template <int SP, bool SPDEL = FA2_SP_DEL>
 __global__ void __launch_bounds__(512)
 fa2_bwd_sp_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                       const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ O,
                       float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV, void* __restrict__ part,
                       long part_stride, int S) {
     __shared__ __attribute__((aligned(16))) char lds[DkdvLds<64, 8, 1, 1, SP>::BYTES];
-    dkdv_body<64, 8, 1, true, 1, true, FA2_IGLP_DKDV, SP>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE,
-                                                           nullptr, dK, dV, S, O, part, part_stride, Delta);
+    dkdv_body<64, 8, 1, true, 1, SPDEL, FA2_IGLP_DKDV, SP>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE,
+                                                            SPDEL ? nullptr : Delta, dK, dV, S, O, part, part_stride,
+                                                            SPDEL ? Delta : nullptr);
 }
 
 // dQ[r][:] = scale * sum over key blocks kb (in order) of part[kb][r][:]; 8 columns per thread
@@ -1988,6 +2004,10 @@ hipError_t FA2_TILE_LAUNCH(launch_backward_ws)(int D, const float* q, const floa
     const long grid = (long)bh * nkb;
     const long pstride = (long)bh * S * D;  // elements per key-block slice
     if (grid > 0x7fffffffL) return hipErrorInvalidValue;
+    if (!FA2_SP_DEL) {
+        const hipError_t e0 = launch_delta(D, dout, o, delta, bh, S, stream);
+        if (e0 != hipSuccess) return e0;
+    }
     if (kind == 1)
         hipLaunchKernelGGL((fa2f16b::fa2_bwd_sp_f16_kernel<1>), dim3((unsigned)grid), dim3(512), 0, stream, q, k, v,
                            dout, lse, o, delta, dk, dv, ws, pstride, S);
