@@ -36,6 +36,9 @@
 #define FA2_TILE_LAUNCH(x) x##_f16
 #define FA2_TILE_HOST(x) x##_fp16
 #endif
+#ifndef FA2_SP_MID
+#define FA2_SP_MID 0  // 1: the previous step's dQ part runs after the step's staging loads are issued
+#endif
 #ifndef FA2_SP_ABL
 #define FA2_SP_ABL 0  // ablation builds (tools/ab_sp_parts.sh): 1 = no dQ product, 2 = no part stores
 #endif
@@ -861,8 +864,12 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         {
             const bool more = it + 1 < nsteps;
             if constexpr (SP) {
-                if (it > 0) dq_part(dsimg + L::DSBUF / 2, it - 1);
-                run_step(smem, smem + QS * TILE, rows[0][0], rows[0][1], it, [&] { if (more) load_next(it + 1); },
+                if (!FA2_SP_MID && it > 0) dq_part(dsimg + L::DSBUF / 2, it - 1);
+                run_step(smem, smem + QS * TILE, rows[0][0], rows[0][1], it,
+                         [&] {
+                             if (more) load_next(it + 1);
+                             if (FA2_SP_MID && it > 0) dq_part(dsimg + L::DSBUF / 2, it - 1);
+                         },
                          ds_write(dsimg));
             } else {
                 run_step(smem, smem + QS * TILE, rows[0][0], rows[0][1], it, [&] { if (more) load_next(it + 1); },
@@ -874,9 +881,13 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         if (it + 1 < nsteps) {
             const bool more = it + 2 < nsteps;
             if constexpr (SP) {
-                dq_part(dsimg, it);
+                if (!FA2_SP_MID) dq_part(dsimg, it);
                 run_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0], rows[1][1], it + 1,
-                         [&] { if (more) load_next(it + 2); }, ds_write(dsimg + L::DSBUF / 2));
+                         [&] {
+                             if (more) load_next(it + 2);
+                             if (FA2_SP_MID) dq_part(dsimg, it);
+                         },
+                         ds_write(dsimg + L::DSBUF / 2));
             } else {
                 run_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0], rows[1][1], it + 1,
                          [&] { if (more) load_next(it + 2); }, NoDsOut());
