@@ -37,7 +37,7 @@
 #define FA2_TILE_HOST(x) x##_fp16
 #endif
 #ifndef FA2_SP_MID
-#define FA2_SP_MID 0  // 1: the previous step's dQ part runs after the step's staging loads are issued
+#define FA2_SP_MID 1  // the previous step's dQ part runs after the step's staging loads are issued (0: before them)
 #endif
 #ifndef FA2_SP_ABL
 #define FA2_SP_ABL 0  // ablation builds (tools/ab_sp_parts.sh): 1 = no dQ product, 2 = no part stores
