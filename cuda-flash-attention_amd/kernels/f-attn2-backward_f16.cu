@@ -1911,8 +1911,9 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
         // profiles/r03/ab/froles/); below 4 the split roles stay (S = 1024: 24.6 vs 33.4)
         const int fqs = tune_knob("BWD_FQS", a >= 4 ? 1 : 2);
         const int fks = tune_knob("BWD_FKS", a >= 4 ? 1 : 2);
-        // waves per workgroup of both roles (8, or 4 for the split pairs)
-        const int fnw = tune_knob("BWD_FNW", tiny ? 4 : 8);
+        // waves per workgroup of both roles (8, or 4 for the split pairs; the unsplit
+        // roles exist at 8 waves only, so a forced FQS = FKS = 1 on a tiny grid takes 8)
+        const int fnw = tune_knob("BWD_FNW", tiny && !(fqs == 1 && fks == 1) ? 4 : 8);
         // an override combination no instance serves is an error, never a silent
         // fallback to the two-kernel plan (an A/B would otherwise time the default)
         const bool forced = tune_knob("BWD_FQS", 0) || tune_knob("BWD_FKS", 0) || tune_knob("BWD_FNW", 0);
