@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--shards-on-device0", type=int, default=0)
     ap.add_argument("--lib", default=None, help="library build to load instead of the in-tree one")
     ap.add_argument("--c5-only", action="store_true")
+    ap.add_argument("--runs", type=int, default=2, help="timed fwd + bwd pairs per C5 entry (medians)")
     args = ap.parse_args()
     import fa2amd
     if args.lib:
@@ -63,10 +64,10 @@ def main():
         fa2amd.tune_set("HOST_CHUNKS", ch)
         out[f"c3_chunks{ch or 'auto'}"] = timed(fa2amd, (4, 16, 2048, 64), 1, 4)
     fa2amd.tune_set(None)
-    out["c5_auto"] = timed(fa2amd, (64, 16, 2048, 64), 1, 2)
+    out["c5_auto"] = timed(fa2amd, (64, 16, 2048, 64), 1, args.runs)
     if args.shards_on_device0:
         fa2amd.tune_set("HOST_SHARDS_ON_DEVICE0", 1)
-        out[f"c5_{args.shards_on_device0}shards_dev0"] = timed(fa2amd, (64, 16, 2048, 64), args.shards_on_device0, 2)
+        out[f"c5_{args.shards_on_device0}shards_dev0"] = timed(fa2amd, (64, 16, 2048, 64), args.shards_on_device0, args.runs)
     fa2amd.tune_set(None)
     fa2amd.host_release()
     print(json.dumps(out, indent=1))
