@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", action="append", default=[], help="alternate libfa2amd.so builds to A/B (repeatable)")
     ap.add_argument("--do", choices=["randn", "ones"], default="randn", help="dO distribution (bench.py uses ones)")
+    ap.add_argument("--inputs", choices=["rand", "spike"], default="rand",
+                    help="Q/K/V U[0,1) as the harness draws them, or with one late spiking key")
     ap.add_argument("--precision", choices=["fp16", "bf16", "fp32"], default="fp16",
                     help="tile precision of the fwd / bwd / stepb calls")
     args = ap.parse_args()
@@ -34,6 +36,11 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(42)
     q, k, v = (torch.rand(B, H, S, D, generator=g).to(dev) for _ in range(3))
+    if args.inputs == "spike":
+        # a late key whose scores sit ~2^18 above the first tile's row max: every query
+        # block's branch-free forward loop notes it and redoes the block with the
+        # rescaling loop (the worst case of the restart, kernel_fa2_optimized_f16.cu)
+        k[:, :, -1, :] = 4.0
     do = torch.randn(B, H, S, D, generator=g).to(dev) if args.do == "randn" else torch.ones(B, H, S, D, device=dev)
     P = args.precision
     o, lse = fa2amd.forward(q, k, v, P)
