@@ -620,11 +620,13 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     }
 
     if (NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    // one staged step out of the current buffers; the next step's loads after QK^T
-    auto step = [&](const _Float16* Kc, const _Float16* Vc, _Float16* Kn, _Float16* Vn, int j, bool more)
-        __attribute__((always_inline)) {
-        const int jj = j * KS + kg;                // this wave's tile
-        const bool live = KS == 1 || jj < ntiles;  // wave-uniform (KS > 1: ragged tail)
+    // one staged step out of the current buffers; the next step's loads after QK^T.
+    // redo (wave-uniform): false for a wave that only stages and keeps its state (the
+    // restart below recomputes just the waves that saw a spike)
+    auto step = [&](const _Float16* Kc, const _Float16* Vc, _Float16* Kn, _Float16* Vn, int j, bool more,
+                    bool redo = true) __attribute__((always_inline)) {
+        const int jj = j * KS + kg;                          // this wave's tile
+        const bool live = (KS == 1 || jj < ntiles) && redo;  // wave-uniform (KS > 1: ragged tail)
         f32x16 sacc[MQ][NKB];
         if (live) fwd_qk<D, MQ, NKB, SEED>(sacc, st, Kc, fo);
         if (more) {
@@ -642,11 +644,11 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         __syncthreads();
     };
     // two steps per trip so every LDS buffer offset is a compile-time immediate
-    auto robust_loop = [&]() __attribute__((always_inline)) {
+    auto robust_loop = [&](bool redo) __attribute__((always_inline)) {
         for (int j = 0; j < nsteps; j += 2) {
-            step(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, j, j + 1 < nsteps);
+            step(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, j, j + 1 < nsteps, redo);
             if (j + 1 < nsteps)
-                step(smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j + 1, j + 2 < nsteps);
+                step(smem + 2 * KS * TILE, smem + 3 * KS * TILE, smem, smem + KS * TILE, j + 1, j + 2 < nsteps, redo);
         }
     };
     // Tile 0 (each key group's first) sets m (the rescaling step); tiles 1.. run the
@@ -711,23 +713,28 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             bad = stepf(MaskTag<1>{}, kc, kc + KS * TILE, smem, smem, jend, false) || bad;
         }
         if (__syncthreads_or(bad)) {
+            // every wave restages; only the waves that saw a spike reset and recompute (the
+            // others' O, l and m never left range and stand as they are)
+            const bool redo = __builtin_amdgcn_readfirstlane(__any(bad) ? 1 : 0) != 0;
+            if (redo) {
 #pragma unroll
-            for (int b = 0; b < D / 32; ++b)
+                for (int b = 0; b < D / 32; ++b)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) st[0].oacc[b][i] = 0.f;  // state only: the Q fragments stay
-            if (SEED) st[0].nm = splat16(0.f);
-            st[0].m = 0.f;
+                    for (int i = 0; i < 16; ++i) st[0].oacc[b][i] = 0.f;  // state only: the Q fragments stay
+                if (SEED) st[0].nm = splat16(0.f);
+                st[0].m = 0.f;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) st[0].l[c] = 0.f;
+                for (int c = 0; c < 4; ++c) st[0].l[c] = 0.f;
+            }
             ks.load(0);
             vs.load(0);
             ks.store(smem, 1.f, tid);
             vs.store(smem + KS * TILE, 1.f, tid);
             __syncthreads();
-            robust_loop();
+            robust_loop(redo);
         }
     } else {
-        robust_loop();
+        robust_loop(true);
     }
     if constexpr (KS > 1) {
         // Key-split merge (the loop ended on a barrier: the tile buffers are free).
