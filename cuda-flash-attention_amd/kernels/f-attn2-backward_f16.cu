@@ -1533,6 +1533,10 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 // writes Δ out), the dK/dV role per step -- so the launch depends on nothing but the
 // forward's outputs: the separate Δ kernel and its launch boundary go away, at the
 // price of the dK/dV role's O reads (these grids are latency-bound, not HBM-bound).
+#ifdef FA2_STAMPS
+#define FA2_STAMP_SLOTS 65536
+__device__ unsigned long long fa2_bwd_stamp_buf[FA2_STAMP_SLOTS][4];
+#endif
 template <int D, int NW, int QS, int KS, int NKB, bool DEL = false>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
@@ -1542,6 +1546,9 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
     constexpr int B1 = DkdvLds<D, NW, 1, QS>::BYTES, B2 = DqLds<D, NW, DEL, NKB, KS>::BYTES;
     __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
     const int b = blockIdx.x;
+#ifdef FA2_STAMPS
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (b < ndk)
         // the dK/dV role with unsplit queries takes the standalone kernel's strategy
         dkdv_body<D, NW, 1, true, QS, DEL, QS == 1 && D == 64 ? FA2_IGLP_DKDV : FA2_IGLP_FUSED>(
@@ -1549,6 +1556,16 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
     else
         dq_body<D, NW, DEL, NKB, true, KS, FA2_IGLP_FUSED>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
                                                            Delta, dQ, S, O);
+#ifdef FA2_STAMPS
+    // timing-only builds: entry, every store of the workgroup complete, role
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0 && b < FA2_STAMP_SLOTS) {
+        fa2_bwd_stamp_buf[b][0] = t0;
+        fa2_bwd_stamp_buf[b][1] = __builtin_amdgcn_s_memrealtime();
+        fa2_bwd_stamp_buf[b][2] = b < ndk ? 0 : 1;
+    }
+#endif
 }
 
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
@@ -2103,3 +2120,15 @@ extern "C" __global__ void D_computation_reduction_kernel_wrapper(const float* d
     fa2f16b::delta_row_body(d_output, output, (long)batch_size * num_heads * seq_len, head_dim, d);
 }
 #endif  // CUPY_INLINE_COMPILE
+
+#if defined(FA2_STAMPS) && !defined(FA2_TILE_BF16) && !defined(CUPY_INLINE_COMPILE)
+// timing-only builds (tools/stamps_small.py): copy the fused backward's per-workgroup
+// stamps [slot][entry, done, role, -] to host memory
+extern "C" int fa2_bwd_stamps_read(void* host, size_t bytes) {
+    if (bytes > sizeof(fa2f16b::fa2_bwd_stamp_buf)) bytes = sizeof(fa2f16b::fa2_bwd_stamp_buf);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(fa2f16b::fa2_bwd_stamp_buf), bytes, 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess
+               ? 0
+               : -1;
+}
+#endif

@@ -534,6 +534,16 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 // NKB 32-key blocks per KV tile (2: 64-key tiles; 1: 32-key tiles, fewer registers
 // for D = 128 at 8 waves).
 //
+// FA2_STAMPS (timing-only builds, tools/stamps_small.py): thread 0 of each workgroup
+// records s_memrealtime (100 MHz) at phase boundaries and writes the stamps over the
+// first 16 floats of its block's first O row at the end (results are then invalid)
+#ifdef FA2_STAMPS
+#define FA2_STAMP(i) \
+    if (tid == 0) stamp[i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define FA2_STAMP(i)
+#endif
+
 // KS > 1 (small grids): the key range is split over KS wave groups of NQ = NW / KS
 // waves.  Wave w handles query rows of slot w % NQ against tiles j·KS + w / NQ;
 // each step stages KS tiles.  The groups' (m, l, O) meet in LDS after the loop
@@ -564,6 +574,10 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     __shared__ __attribute__((aligned(16))) float ostage[NQ][32][36];  // per-wave O block stage
 
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+#ifdef FA2_STAMPS
+    unsigned long long stamp[8] = {};
+#endif
+    FA2_STAMP(0);
     const int wave = KS > 1 ? (tid >> 6) % NQ : tid >> 6;  // query slot of the wave
     const int kg = KS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NQ) : 0;  // key group
     const int nqb = (S + QW * NQ - 1) / (QW * NQ);
@@ -603,6 +617,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             vs.store(smem + KS * TILE, 1.f, tid);
         }
         __syncthreads();
+        FA2_STAMP(1);
         fwd_init<D, SEED>(st[0], nullptr, 0, S, S, h);  // state only (q >= S: no Q read)
 #pragma unroll
         for (int t = 0; t < D / 16; ++t) st[0].qf[t] = fo.rowop(qblk, wave * QW, t);
@@ -690,7 +705,9 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             __syncthreads();
             return b;
         };
+        FA2_STAMP(2);
         step(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, 0, 1 < nsteps);
+        FA2_STAMP(3);
         // D <= 64: the ragged last tile's step (always the last one) runs after the loop
         // (r03 A/B: B2_H8 fwd S = 512 -7 %, S = 1024 -5 %, C3 -1.2 %); D = 128 keeps it
         // in the loop (peeled, its 32-key-tile loop ran 5.8 % slower at C4)
@@ -712,6 +729,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             _Float16* const kc = (jend & 1) ? smem + 2 * KS * TILE : smem;
             bad = stepf(MaskTag<1>{}, kc, kc + KS * TILE, smem, smem, jend, false) || bad;
         }
+        FA2_STAMP(4);
         if (__syncthreads_or(bad)) {
             // every wave restages; only the waves that saw a spike reset and recompute (the
             // others' O, l and m never left range and stand as they are)
@@ -769,6 +787,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         st[0].l[0] = l;
         st[0].l[1] = st[0].l[2] = st[0].l[3] = 0.f;
     }
+    FA2_STAMP(5);
     // O through a wave-private LDS stage, one 32x32 block at a time, stored as whole
     // 128-B row segments (8 rows per instruction) instead of 16-B pieces of 32 rows
     {
@@ -791,6 +810,16 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         }
         if (h == 0 && q0 < S) LSE[(long)bh * S + q0] = st[0].m * FA2_LN2 + __logf(lt);
     }
+#ifdef FA2_STAMPS
+    FA2_STAMP(6);
+    __builtin_amdgcn_s_waitcnt(0);  // every store of this wave complete
+    FA2_STAMP(7);
+    if (tid == 0) {
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(O + base + (long)qb * QW * NQ * D);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dst[i] = stamp[i];
+    }
+#endif
 }
 
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
