@@ -38,7 +38,7 @@ C_SYMBOLS = (
     "fa2_version", "fa2_build_id", "fa2_device_count",
 )
 # launch-plan overrides fa2_tune_set accepts (include/fa2_amd.h)
-KNOBS = ("FWD_WAVES", "FWD_KS", "DKDV_WAVES", "DKDV_QS", "DQ_WAVES", "DQ_KS", "BWD_FUSED", "BWD_FUSED_DELTA",
+KNOBS = ("FWD_WAVES", "FWD_KS", "FWD_NKB", "DKDV_WAVES", "DKDV_QS", "DQ_WAVES", "DQ_KS", "BWD_FUSED", "BWD_FUSED_DELTA",
          "BWD_FQS", "BWD_FKS", "BWD_FNW", "DQ_PIPE", "BWD_SP", "BWD_SP_NORED", "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS")
 
 

@@ -150,4 +150,7 @@ int tune_knob(const char* name, int dflt);
 // to themselves); maxnw when even that grid fills the chip.
 int auto_waves(long blocks32, int maxnw, int minnw = 2);
 
+// Compute units of the current device (cached per device).
+int cu_count();
+
 }  // namespace fa2

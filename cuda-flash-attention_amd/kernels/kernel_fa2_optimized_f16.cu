@@ -930,16 +930,40 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     // bwd step, 15 rounds: B2_H8_S2048 100.6 -> 99.3 us with dO = ones, 104.3 -> 103.1
     // with dO ~ N(0,1)); D = 32 stays unsplit at 4 waves (the split measured +5.5 %).
     int ks = tune_knob("FWD_KS", 0);
-    if (ks == 0 && nw == 0 && D <= 64 && auto_waves(units, 8) == 2) {
+    // FWD_NKB (0 = auto): 32-key (1) or 64-key (2) tiles of a key-split plan
+    int nkb = tune_knob("FWD_NKB", 0);
+    if (ks == 0 && nw == 0 && D == 64 && units < 8L * cu_count()) {
+        // D = 64 on fewer than 8 blocks of 32 rows per CU: the fewest query rows per
+        // workgroup whose grid still runs in ONE round of workgroups (one per CU; every
+        // workgroup streams its head's whole K/V, so a second round costs a whole
+        // workgroup time): 32 rows (4 waves, KS = 4), 64 (8 waves, KS = 4), 128 (8
+        // waves, KS = 2), else the unsplit 256-row plan.  r04 (in-process A/B,
+        // profiles/r04/nkb/): B2_H8_S1500 fwd 31.5 -> 19.1 us (the previous rule took
+        // KS = 4 on 64 rows: 376 workgroups, two rounds); S = 512 / 1024 / 2048 and
+        // B4_H8_S1024 pick the plans they had.
+        const long ncu = cu_count();
+        if (units <= ncu) {
+            ks = 4, nw = 4;
+        } else if ((units + 1) / 2 <= ncu) {
+            ks = 4, nw = 8;
+        } else if ((units + 3) / 4 <= ncu) {
+            ks = 2, nw = 8;
+        } else {
+            nw = 8;
+        }
+    } else if (ks == 0 && nw == 0 && D <= 64 && auto_waves(units, 8) == 2) {
         ks = 4;
         nw = auto_waves(units, 2, 1) == 2 ? 8 : 4;
-    } else if (ks == 0 && nw == 0 && D == 64 && auto_waves(units, 8) == 4) {
-        ks = 2;
-        nw = 8;
     }
     if (nw == 0) nw = auto_waves(units, 8);
     if constexpr (D <= 64) {
-        if (ks == 2 && nw == 8) return fwd_f16_launch<D, 8, 2>(q, k, v, o, lse, bh, S, stream);
+        // KS = 2 at 8 waves on 64-key tiles (D = 64, r04: 249 VGPRs, no spill; twice the
+        // MFMAs per barrier of the 32-key tiles): B2_H8_S2048 fwd 29.6 -> 25.4 us, step
+        // 99.1 -> 95.7; B4_H8_S1024 fwd 18.1 -> 15.8; S = 1500 22.3 -> 19.1
+        // (profiles/r04/nkb/).  KS = 4 keeps 32-key tiles at 8 waves (64-key tiles spill).
+        if (ks == 2 && nw == 8 && nkb != 1) return fwd_f16_launch<D, 8, 2, 2>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 2 && nw == 8) return fwd_f16_launch<D, 8, 2, 1>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 4 && nw == 4 && nkb == 2) return fwd_f16_launch<D, 4, 4, 2>(q, k, v, o, lse, bh, S, stream);
         if (ks == 4 && nw == 8) return fwd_f16_launch<D, 8, 4>(q, k, v, o, lse, bh, S, stream);
         if (ks == 4 && nw == 4) return fwd_f16_launch<D, 4, 4>(q, k, v, o, lse, bh, S, stream);
         if (ks == 2 && nw == 4) return fwd_f16_launch<D, 4, 2>(q, k, v, o, lse, bh, S, stream);

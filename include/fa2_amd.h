@@ -137,7 +137,7 @@ int fa2_shard_range(int total_heads, int shards, int index, int* first, int* cou
 /* Launch-plan override (tests and tuning tools only; nothing is read from the
  * environment).  fa2_tune_set("DKDV_QS", 2) makes the next launches use that plan
  * where the shape allows it; fa2_tune_set(NULL, 0) clears every override.  Knobs:
- * FWD_WAVES, FWD_KS, DKDV_WAVES, DKDV_QS, DQ_WAVES, DQ_KS, BWD_FUSED,
+ * FWD_WAVES, FWD_KS, FWD_NKB, DKDV_WAVES, DKDV_QS, DQ_WAVES, DQ_KS, BWD_FUSED,
  * BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW, DQ_PIPE, BWD_SP (see the launchers in
  * kernels/), and
  * the test-only HOST_SHARDS_ON_DEVICE0 = 1 (fa2_*_host run every shard on device 0,
