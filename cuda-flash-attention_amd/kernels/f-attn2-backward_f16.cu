@@ -1926,8 +1926,14 @@ hipError_t fused_dispatch(const float* q, const float* k, const float* v, const 
         // fused kernel: B2_H8_S2048 bwd 69.0 -> 64.4 us, dO ~ N(0,1) 72.7 -> 68.0, S = 1500
         // 54.3 -> 48.7, B4_H8_S1024 43.9 -> 39.6, D = 32 S = 2048 44.3 -> 41.6;
         // profiles/r03/ab/froles/); below 4 the split roles stay (S = 1024: 24.6 vs 33.4)
-        const int fqs = tune_knob("BWD_FQS", a >= 4 ? 1 : 2);
-        const int fks = tune_knob("BWD_FKS", a >= 4 ? 1 : 2);
+        // r04: the split roles (128 keys / 128 query rows per workgroup: units / 2
+        // workgroups) only while their grid fits one round of workgroups; past that the
+        // unsplit roles (units / 4) win: B2_H8_S1500 bwd 54.5 -> 47.3 us, B3_H8_S1024
+        // 41.0 -> 36.2; B2_H8_S1024 (exactly one round split) keeps the split, 26.2 vs
+        // 34.0 unsplit (profiles/r04/bwdr/)
+        const bool split = (units + 1) / 2 <= (long)cu_count();
+        const int fqs = tune_knob("BWD_FQS", split ? 2 : 1);
+        const int fks = tune_knob("BWD_FKS", split ? 2 : 1);
         // waves per workgroup of both roles (8, or 4 for the split pairs; the unsplit
         // roles exist at 8 waves only, so a forced FQS = FKS = 1 on a tiny grid takes 8)
         const int fnw = tune_knob("BWD_FNW", tiny && !(fqs == 1 && fks == 1) ? 4 : 8);
