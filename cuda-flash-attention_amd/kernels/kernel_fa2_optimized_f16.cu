@@ -920,27 +920,24 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     // over the grid of 32-query wave units), FWD_KS.
     const long units = (long)bh * ((S + 31) / 32);
     int nw = tune_knob("FWD_WAVES", 0);
-    // Key groups per workgroup (0 = auto).  Auto: where even 4-wave
-    // workgroups would leave CUs idle (< 4 query blocks per CU), split the key range
-    // 4 ways instead of shrinking the workgroup -- 8 waves on 64 query rows, or 4 waves
-    // on 32 rows below 2 query blocks per CU.  Measured (B2_H8_D64 fwd, r01):
-    // S = 512 12.4 -> 9.9 us, S = 1024 21.4 -> 15.4 us; at S = 2048 (4 blocks per CU)
-    // KS = 2 on 32-key tiles tied the unsplit 4-wave kernel in r01 (35.9 vs 34.8 us).
-    // With 4-8 blocks per CU, D = 64 splits the key range 2 ways at 8 waves (r02, fwd +
-    // bwd step, 15 rounds: B2_H8_S2048 100.6 -> 99.3 us with dO = ones, 104.3 -> 103.1
-    // with dO ~ N(0,1)); D = 32 stays unsplit at 4 waves (the split measured +5.5 %).
+    // Key groups per workgroup (0 = auto).  Small grids split the key range over wave
+    // groups instead of shrinking the workgroup (r01, B2_H8_D64 fwd: S = 512 12.4 -> 9.9
+    // us, S = 1024 21.4 -> 15.4; r02: KS = 2 at 8 waves on B2_H8_S2048, step 100.6 ->
+    // 99.3 us); r04 picks the split by workgroup rounds (below).
     int ks = tune_knob("FWD_KS", 0);
     // FWD_NKB (0 = auto): 32-key (1) or 64-key (2) tiles of a key-split plan
     int nkb = tune_knob("FWD_NKB", 0);
-    if (ks == 0 && nw == 0 && D == 64 && units < 8L * cu_count()) {
-        // D = 64 on fewer than 8 blocks of 32 rows per CU: the fewest query rows per
+    if (ks == 0 && nw == 0 && D <= 64 && units < 8L * cu_count()) {
+        // D <= 64 on fewer than 8 blocks of 32 rows per CU: the fewest query rows per
         // workgroup whose grid still runs in ONE round of workgroups (one per CU; every
         // workgroup streams its head's whole K/V, so a second round costs a whole
         // workgroup time): 32 rows (4 waves, KS = 4), 64 (8 waves, KS = 4), 128 (8
         // waves, KS = 2), else the unsplit 256-row plan.  r04 (in-process A/B,
         // profiles/r04/nkb/): B2_H8_S1500 fwd 31.5 -> 19.1 us (the previous rule took
         // KS = 4 on 64 rows: 376 workgroups, two rounds); S = 512 / 1024 / 2048 and
-        // B4_H8_S1024 pick the plans they had.
+        // B4_H8_S1024 pick the plans they had.  D = 32 (which ran unsplit 4-wave
+        // workgroups at 4-8 blocks per CU): S = 1500 20.0 -> 14.4 us, S = 2048 21.1 ->
+        // 17.5, S = 3000 38.3 -> 37.6 (profiles/r04/d32/).
         const long ncu = cu_count();
         if (units <= ncu) {
             ks = 4, nw = 4;
@@ -951,9 +948,6 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
         } else {
             nw = 8;
         }
-    } else if (ks == 0 && nw == 0 && D <= 64 && auto_waves(units, 8) == 2) {
-        ks = 4;
-        nw = auto_waves(units, 2, 1) == 2 ? 8 : 4;
     }
     if (nw == 0) nw = auto_waves(units, 8);
     if constexpr (D <= 64) {
