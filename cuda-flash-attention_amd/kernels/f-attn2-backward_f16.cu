@@ -1786,7 +1786,10 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
         else if (a == 2 && D <= 32) qs = 4, nw = 8;
         else if (a == 2) qs = 2, nw = 4;
     }
-    if (nw == 0) nw = auto_waves(units, D <= 64 ? 8 : 4);
+    // D = 128: 4 waves on every grid (r04: the 2-wave workgroups auto_waves gave small
+    // grids measured slower everywhere, B2_H8 D = 128 dK/dV S = 1500 87.9 -> 73.5 us,
+    // 1024 54.3 -> 50.9, 512 29.0 -> 28.1; profiles/r04/d128/)
+    if (nw == 0) nw = D <= 64 ? auto_waves(units, 8) : 4;
     if constexpr (D <= 64) {
         if (qs == 2 && nw == 8) return dkdv_launch<D, 8, true, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
         if (qs == 2 && nw == 4) return dkdv_launch<D, 4, true, 2>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);

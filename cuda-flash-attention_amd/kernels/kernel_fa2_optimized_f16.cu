@@ -949,6 +949,11 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
             nw = 8;
         }
     }
+    // D = 128 on small grids: 4 waves up to one 32-row block per CU, else 8 -- fewer,
+    // larger workgroups than auto_waves' 2-wave ones, each streaming its head's K/V once
+    // for more rows (r04, B2_H8 D = 128 fwd: S = 512 21.0 -> 19.2 us, 1024 37.5 -> 32.9,
+    // 1500 56.7 -> 47.0, 2048 65.9 -> 61.8; profiles/r04/d128/)
+    if (ks == 0 && nw == 0 && D == 128 && units < 8L * cu_count()) nw = units <= cu_count() ? 4 : 8;
     if (nw == 0) nw = auto_waves(units, 8);
     if constexpr (D <= 64) {
         // KS = 2 at 8 waves on 64-key tiles (D = 64, r04: 249 VGPRs, no spill; twice the
