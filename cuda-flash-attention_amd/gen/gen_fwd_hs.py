@@ -1,0 +1,685 @@
+#!/usr/bin/env python3
+"""Generator of the hand-scheduled FA2 forward tile loop for gfx950 (MI355X).
+
+Writes ../kernels/fa2_fwd_hs.inc: one inline-asm body per (head_dim, tile type) that the
+kernel `fa2_fwd_hs_kernel<D>` (kernel_fa2_optimized_f16.cu) runs between its C++
+prologue (Q block and the first K/V tile staged into LDS) and its C++ epilogue (O rows
+normalised and stored from an LDS stage, LSE).  It is the forward of the reference's
+`flash_attention2_forward_kernel_fp16` (kernels/kernel_fa2_optimized_f16.cu:97-330):
+S = Q Kᵀ / √D, online softmax, O += P V, LSE -- on a different structure:
+
+  * one workgroup = 4 waves = 256 query rows, ONE wave per SIMD with the whole
+    512-register file; each wave holds 64 query rows as two 32-row chains A and B
+    (cdna_hip_programming.md, attention forward "4-wave, one-wave-per-SIMD");
+  * per 64-key tile the wave runs four phases, each one MFMA chain with the other
+    chain's softmax placed in its gaps:
+        P1  QKᵀ of A (tile j)   | softmax of B (tile j-1), second half
+        P2  PV   of B (tile j-1)| softmax of A (tile j),   first half
+        P3  QKᵀ of B (tile j)   | softmax of A (tile j),   second half   -> barrier
+        P4  PV   of A (tile j)  | softmax of B (tile j),   first half
+    so the matrix pipe is never waiting for the exponentials of the chain it works on;
+  * every filler (exp, cvt, add, LDS fragment read, staging load / convert / LDS write)
+    is assigned to an MFMA gap by the list scheduler below, with per-gap issue budgets
+    and at most EXP_PER_GAP v_exp per gap; waits are counted (s_waitcnt lgkmcnt / vmcnt
+    with the exact count of younger operations) and hazard wait states are inserted
+    from the gfx950 rules (MFMA 8-pass result -> any other reader 12 states, VALU ->
+    MFMA operand 2, transcendental -> VALU 1);
+  * K and V tiles are fp32 in HBM (the reference's layout): staged one tile ahead through
+    registers (buffer loads with a hardware range check) -> fp16/bf16 -> XOR-swizzled LDS
+    (the swizzle of kernel_fa2_optimized_f16.cu, conflict-free for both fragment reads);
+  * m (row reference, log2 units) is the first tile's row max and moves only through the
+    robust C++ path: every tile's half-row sums are checked against 2^13 (the fp16 range
+    guard of the library's other forward kernels); a flagged block is recomputed.
+
+Register map (per wave, D = head dim, NB = D/32, NTQ = D/16, CPT = D/32):
+  AGPR  O[c][b]      a[16(c*NB+b)]            output accumulators (C = D in AGPRs)
+        Q[c][t]      a[32NB + 4(c*NTQ+t)]     Q fragments (B operand of Sᵀ = K Qᵀ)
+        Vf[i]        a[32NB+8NTQ + 4i]        Vᵀ fragments of one tile (A operand of PV)
+  VGPR  S[c][kb]     v[32c + 16kb]            Sᵀ accumulators; exps and packed P in place
+        NM[c]        v[64 + 16c]              -m splat: the C operand of each QKᵀ chain
+        Kf ring      v[96 + 4r], r < 8        K fragments (A operand of QKᵀ)
+        staging      v[128 ...]               fp32 K then V rows of the next tile
+        misc         m, l, tile partial sums, temporaries
+
+Usage: python3 gen_fwd_hs.py [--check]   (--check: verify the .inc is up to date)
+"""
+import os
+import sys
+
+KT = 64  # keys per tile
+NWAVE = 4
+ROWS = 64 * NWAVE  # query rows per workgroup
+SUM_MAX_BITS = 0x46000000  # 8192.0f: half-row tile-sum guard (FA2_TILE_SUM_MAX)
+
+
+# ---------------------------------------------------------------------------------------
+# instructions
+# ---------------------------------------------------------------------------------------
+class Ins:
+    """One instruction: text, class, registers read (with MFMA operand role) and written."""
+
+    __slots__ = ("text", "kind", "rd", "wr", "cost", "earliest", "deadline", "trans", "perm")
+
+    def __init__(self, text, kind, rd=(), wr=(), cost=None, earliest=0, deadline=None):
+        self.text = text
+        self.kind = kind  # mfma valu exp dsr dsw vmem salu wait nop bar label branch
+        self.rd = list(rd)  # list of (reg, role)
+        self.wr = list(wr)
+        self.earliest = earliest
+        self.deadline = deadline
+        self.trans = kind == "exp"
+        self.perm = text.startswith("v_permlane")
+        if cost is None:
+            cost = {"mfma": 8, "exp": 8, "valu": 4, "dsr": 4, "dsw": 8, "vmem": 4, "salu": 2, "wait": 0,
+                    "nop": 4, "bar": 4, "label": 0, "branch": 4}[kind]
+        self.cost = cost
+
+    def ws(self):
+        """wait states this instruction provides to a later hazard consumer"""
+        if self.kind == "label":
+            return 0
+        if self.kind == "nop":
+            return int(self.text.split()[1]) + 1
+        return 1
+
+
+def rng(p, base, n):
+    return [f"{p}{base + i}" for i in range(n)]
+
+
+def rtxt(p, base, n):
+    return f"{p}{base}" if n == 1 else f"{p}[{base}:{base + n - 1}]"
+
+
+def R(regs, role="x"):
+    return [(r, role) for r in regs]
+
+
+# ---------------------------------------------------------------------------------------
+# configuration and register map
+# ---------------------------------------------------------------------------------------
+class Cfg:
+    def __init__(self, D, bf16):
+        self.D, self.bf16 = D, bf16
+        self.NB, self.NTQ, self.CPT = D // 32, D // 16, D // 32
+        self.NF = 4 * self.NB  # V fragments per tile
+        self.NKF = 2 * self.NTQ  # K fragments per tile
+        self.ring = 8  # K fragment ring slots
+        self.keep_k = self.NKF <= self.ring  # D = 64: all K fragments stay for both QKᵀ
+        self.QB = 32 * self.NB
+        self.VB = self.QB + 8 * self.NTQ
+        self.nagpr = self.VB + 4 * self.NF
+        self.STG = 128
+        self.MB = self.STG + 16 * self.CPT
+        self.nvgpr = self.MB + 16
+        self.TBB = KT * D * 2  # bytes of one fp16 tile image
+        self.OST = D + 4  # O stage row stride (floats)
+        self.mf = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
+        self.cvt = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
+        self.exp_per_gap = 2 if D <= 64 else 1
+
+    # AGPRs
+    def O(self, c, b):
+        return 16 * (c * self.NB + b)
+
+    def Q(self, c, t):
+        return self.QB + 4 * (c * self.NTQ + t)
+
+    def Vf(self, i):
+        return self.VB + 4 * i
+
+    # VGPRs
+    def S(self, c, kb, i=0):
+        return 32 * c + 16 * kb + i
+
+    def NM(self, c):
+        return 64 + 16 * c
+
+    def Kr(self, r):
+        return 96 + 4 * r
+
+    def stg(self, tensor, cc):
+        return self.STG + 8 * (tensor * self.CPT + cc)
+
+    def m(self, c):
+        return self.MB + c
+
+    def l(self, c):
+        return self.MB + 2 + c
+
+    def T(self, c, k):
+        return self.MB + 4 + 4 * c + k
+
+    def ts(self, c):
+        return self.MB + 12 + c
+
+    def tmp(self, k):
+        return self.MB + 14 + k
+
+    # LDS byte offsets
+    def koff(self, slot):
+        return slot * self.TBB
+
+    def voff(self, slot):
+        return (2 + slot) * self.TBB
+
+    @property
+    def lds_bytes(self):
+        return max(8 * self.TBB, ROWS * self.OST * 4)
+
+    def vfrag_addr(self, i):
+        b, kb, s = i // 4, (i // 2) % 2, i % 2
+        return b, (kb * 32 + 16 * s) * self.D * 2
+
+
+# ---------------------------------------------------------------------------------------
+# instruction builders
+# ---------------------------------------------------------------------------------------
+def mfma(cfg, dst, a, b, c, c_is_zero=False):
+    """dst/c: ('v'|'a', base) 16-reg tuples; a/b: ('v'|'a', base) 4-reg tuples"""
+    rd = R(rng(a[0], a[1], 4), "A") + R(rng(b[0], b[1], 4), "B")
+    if not c_is_zero:
+        rd += R(rng(c[0], c[1], 16), "C")
+    ctxt = "0" if c_is_zero else rtxt(c[0], c[1], 16)
+    text = f"{cfg.mf} {rtxt(dst[0], dst[1], 16)}, {rtxt(a[0], a[1], 4)}, {rtxt(b[0], b[1], 4)}, {ctxt}"
+    return Ins(text, "mfma", rd, rng(dst[0], dst[1], 16))
+
+
+def valu(text, rd, wr, kind="valu"):
+    return Ins(text, kind, R(rd), wr)
+
+
+def kfrag_read(cfg, f, slot, dst):
+    kb, t = f // cfg.NTQ, f % cfg.NTQ
+    off = cfg.koff(slot) + kb * 32 * cfg.D * 2
+    return Ins(f"ds_read_b128 {rtxt('v', dst, 4)}, %[ka{t}] offset:{off}", "dsr", [], rng("v", dst, 4))
+
+
+def vfrag_reads(cfg, i, slot, earliest=0):
+    b, off = cfg.vfrag_addr(i)
+    off += cfg.voff(slot)
+    d = cfg.Vf(i)
+    return [
+        Ins(f"ds_read_b64_tr_b16 {rtxt('a', d, 2)}, %[va{b}_0] offset:{off}", "dsr", [], rng("a", d, 2),
+            earliest=earliest),
+        Ins(f"ds_read_b64_tr_b16 {rtxt('a', d + 2, 2)}, %[va{b}_1] offset:{off}", "dsr", [], rng("a", d + 2, 2),
+            earliest=earliest),
+    ]
+
+
+def qk_mfmas(cfg, c, kreg):
+    """Sᵀ[c] = K Qᵀ[c] - m[c]: kb-major chains (kb = 0 finishes first)"""
+    out = []
+    for kb in range(2):
+        for t in range(cfg.NTQ):
+            f = kb * cfg.NTQ + t
+            cc = ("v", cfg.NM(c)) if t == 0 else ("v", cfg.S(c, kb))
+            out.append(mfma(cfg, ("v", cfg.S(c, kb)), ("v", kreg(f)), ("a", cfg.Q(c, t)), cc))
+    return out
+
+
+def qk_mfmas_zero(cfg, c, kreg):
+    out = []
+    for kb in range(2):
+        for t in range(cfg.NTQ):
+            f = kb * cfg.NTQ + t
+            out.append(mfma(cfg, ("v", cfg.S(c, kb)), ("v", kreg(f)), ("a", cfg.Q(c, t)), ("v", cfg.S(c, kb)),
+                            c_is_zero=(t == 0)))
+    return out
+
+
+def pv_mfmas(cfg, c, first=False):
+    """Oᵀ[c][b] += Vᵀ Pᵀ[c]: b-major, so Vf slot i is free after MFMA i"""
+    out = []
+    for b in range(cfg.NB):
+        for kb in range(2):
+            for s in range(2):
+                i = b * 4 + kb * 2 + s
+                z = first and kb == 0 and s == 0
+                out.append(mfma(cfg, ("a", cfg.O(c, b)), ("a", cfg.Vf(i)), ("v", cfg.S(c, kb, 8 * s)),
+                                ("a", cfg.O(c, b)), c_is_zero=z))
+    return out
+
+
+def softmax_part(cfg, c, kb, final):
+    """exp2 of the 16 scores of half kb (in place), partial row sums, pack to 16-bit P (in place)"""
+    out = []
+    S = lambda i: cfg.S(c, kb, i)
+    for s in range(2):
+        for i in range(8 * s, 8 * s + 8):
+            out.append(valu(f"v_exp_f32 v{S(i)}, v{S(i)}", [f"v{S(i)}"], [f"v{S(i)}"], kind="exp"))
+        for k in range(4):
+            T = cfg.T(c, k)
+            if kb == 0 and s == 0:
+                out.append(valu(f"v_add_f32 v{T}, v{S(k)}, v{S(k + 4)}", [f"v{S(k)}", f"v{S(k + 4)}"], [f"v{T}"]))
+            else:
+                for e in (8 * s + k, 8 * s + k + 4):
+                    out.append(valu(f"v_add_f32 v{T}, v{T}, v{S(e)}", [f"v{T}", f"v{S(e)}"], [f"v{T}"]))
+        for ii in range(4):
+            d, a, b = S(8 * s + ii), S(8 * s + 2 * ii), S(8 * s + 2 * ii + 1)
+            out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
+    if final:
+        T = [cfg.T(c, k) for k in range(4)]
+        ts = cfg.ts(c)
+        out.append(valu(f"v_add_f32 v{T[0]}, v{T[0]}, v{T[1]}", [f"v{T[0]}", f"v{T[1]}"], [f"v{T[0]}"]))
+        out.append(valu(f"v_add_f32 v{T[2]}, v{T[2]}, v{T[3]}", [f"v{T[2]}", f"v{T[3]}"], [f"v{T[2]}"]))
+        out.append(valu(f"v_add_f32 v{ts}, v{T[0]}, v{T[2]}", [f"v{T[0]}", f"v{T[2]}"], [f"v{ts}"]))
+        out.append(valu(f"v_add_f32 v{cfg.l(c)}, v{cfg.l(c)}, v{ts}", [f"v{cfg.l(c)}", f"v{ts}"], [f"v{cfg.l(c)}"]))
+        # NaN or a half-row sum above 2^13 -> the block is recomputed by the robust path
+        out.append(valu(f"v_cmp_nle_f32 vcc, {SUM_MAX_BITS:#x}, v{ts}", [f"v{ts}"], ["vcc"]))
+        out.append(Ins("s_or_b64 %[flg], %[flg], vcc", "salu", R(["vcc", "s:flg"]), ["s:flg"]))
+    return out
+
+
+def staging_loads(cfg, tensor):
+    rs = "%[rsk]" if tensor == 0 else "%[rsv]"
+    out = []
+    for cc in range(cfg.CPT):
+        base = cfg.stg(tensor, cc)
+        for h in range(2):
+            off = f" offset:{16 * h}" if h else ""
+            out.append(Ins(f"buffer_load_dwordx4 {rtxt('v', base + 4 * h, 4)}, %[vo{cc}], {rs}, %[goff] offen{off}",
+                           "vmem", R(["s:goff"]), rng("v", base + 4 * h, 4)))
+    return out
+
+
+def goff_inc(cfg):
+    return Ins(f"s_add_u32 %[goff], %[goff], {KT * cfg.D * 4}", "salu", R(["s:goff"]), ["s:goff", "scc"])
+
+
+def staging_convert(cfg, tensor, slot):
+    out = []
+    toff = cfg.koff(slot) if tensor == 0 else cfg.voff(slot)
+    rows_per_chunk_step = 256 // (cfg.D // 8)
+    for cc in range(cfg.CPT):
+        base = cfg.stg(tensor, cc)
+        for ii in range(4):
+            d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
+            out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
+        off = toff + cc * rows_per_chunk_step * cfg.D * 2
+        out.append(Ins(f"ds_write_b128 %[lo], {rtxt('v', base, 4)} offset:{off}", "dsw", R(rng("v", base, 4)), []))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# list scheduler: MFMA gaps <- filler streams
+# ---------------------------------------------------------------------------------------
+def schedule_phase(cfg, mfmas, streams, name, log):
+    nM = len(mfmas)
+    streams = [s for s in streams if s]
+    pos = [0] * len(streams)
+    tot = [max(1, sum(i.cost for i in s)) for s in streams]
+    done = [0] * len(streams)
+    total = sum(sum(i.cost for i in s) for s in streams)
+    cap = max(24, -(-total // max(1, nM)))
+    out = []
+    for g in range(nM + 1):
+        used = 0
+        nexp = 0
+        while True:
+            cands = [k for k, s in enumerate(streams) if pos[k] < len(s) and s[pos[k]].earliest <= g]
+            if not cands:
+                break
+            forced = [k for k in cands if streams[k][pos[k]].deadline is not None and streams[k][pos[k]].deadline <= g]
+            if forced:
+                k = min(forced, key=lambda k: streams[k][pos[k]].deadline)
+            else:
+                if g < nM and used >= cap:
+                    break
+                ok = [k for k in cands if g == nM or not (streams[k][pos[k]].kind == "exp" and nexp >= cfg.exp_per_gap)]
+                if not ok:
+                    break
+                k = min(ok, key=lambda k: (done[k] / tot[k], k))
+            ins = streams[k][pos[k]]
+            pos[k] += 1
+            done[k] += ins.cost
+            used += ins.cost
+            nexp += ins.kind == "exp"
+            out.append(ins)
+        if g < nM:
+            out.append(mfmas[g])
+    for k, s in enumerate(streams):
+        assert pos[k] == len(s), f"{name}: stream {k} not drained"
+    nexp = sum(1 for s in streams for i in s if i.kind == "exp")
+    nfill = sum(len(s) for s in streams)
+    log.append(f"  {name:4s}: {nM:2d} MFMA, {nfill:3d} fillers ({nexp} exp), filler issue {total:4d} cyc, "
+               f"cap/gap {cap}, est. {max(32 * nM, total + 8 * nM)} cyc")
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# program pieces
+# ---------------------------------------------------------------------------------------
+def body(cfg, p, log):
+    """one 64-key tile j with parity p: K/V of tile j in slot p; tile j+1 staged into 1-p"""
+    q = 1 - p
+    NKF, NTQ = cfg.NKF, cfg.NTQ
+    ring = lambda f: cfg.Kr(f % cfg.ring)
+    seq = []
+    # P1: QKᵀ of chain A (tile j) | softmax B (j-1) second half, K fragments 8.. (D=128), stage K(j+1)
+    kreads = []
+    if not cfg.keep_k:
+        for f in range(cfg.ring, NKF):
+            r = f - cfg.ring
+            ins = kfrag_read(cfg, f, p, cfg.Kr(r))
+            ins.earliest, ins.deadline = r + 1, f - 3
+            kreads.append(ins)
+    conv = staging_convert(cfg, 0, q)
+    for ins in conv:
+        ins.earliest = len(qk_mfmas(cfg, 0, ring)) // 4
+    seq += schedule_phase(cfg, qk_mfmas(cfg, 0, ring), [softmax_part(cfg, 1, 1, True), kreads, conv], f"P1.{p}", log)
+    # P2: PV of chain B (tile j-1) | softmax A (j) first half, V(j+1) staged, K(j+2) loads,
+    #     K re-read 0..7 (D=128), first V(j) fragments into freed Vf slots
+    nsplit = cfg.NF // 4 if cfg.D > 64 else 0
+    vre = []
+    for i in range(nsplit):
+        vre += vfrag_reads(cfg, i, p, earliest=i + 2)
+    rer = [] if cfg.keep_k else [kfrag_read(cfg, f, p, cfg.Kr(f)) for f in range(cfg.ring)]
+    seq += schedule_phase(cfg, pv_mfmas(cfg, 1), [softmax_part(cfg, 0, 0, False), staging_convert(cfg, 1, q),
+                                                  staging_loads(cfg, 0), rer, vre], f"P2.{p}", log)
+    # P3: QKᵀ of chain B (tile j) | softmax A (j) second half, K fragments 8.. (D=128), rest of V(j)
+    kreads = []
+    if not cfg.keep_k:
+        for f in range(cfg.ring, NKF):
+            r = f - cfg.ring
+            ins = kfrag_read(cfg, f, p, cfg.Kr(r))
+            ins.earliest, ins.deadline = r + 1, f - 3
+            kreads.append(ins)
+    vre = []
+    for i in range(nsplit, cfg.NF):
+        vre += vfrag_reads(cfg, i, p)
+    seq += schedule_phase(cfg, qk_mfmas(cfg, 1, ring), [softmax_part(cfg, 0, 1, True), kreads, vre], f"P3.{p}", log)
+    seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
+    seq.append(Ins("s_barrier", "bar"))
+    # P4: PV of chain A (tile j) | softmax B (j) first half, K(j+1) fragment prefetch, V(j+2) loads
+    pre = [kfrag_read(cfg, f, q, cfg.Kr(f)) for f in range(min(cfg.ring, NKF))]
+    seq += schedule_phase(cfg, pv_mfmas(cfg, 0), [softmax_part(cfg, 1, 0, False), pre,
+                                                  staging_loads(cfg, 1) + [goff_inc(cfg)]], f"P4.{p}", log)
+    return seq
+
+
+def prologue(cfg):
+    D, NTQ, NKF = cfg.D, cfg.NTQ, cfg.NKF
+    seq = [Ins("s_mov_b64 %[flg], 0", "salu", [], ["s:flg"]),
+           valu(f"v_mov_b32 v{cfg.l(0)}, 0", [], [f"v{cfg.l(0)}"]),
+           valu(f"v_mov_b32 v{cfg.l(1)}, 0", [], [f"v{cfg.l(1)}"])]
+    # tile 1 loads (K then V)
+    seq += staging_loads(cfg, 0) + staging_loads(cfg, 1) + [goff_inc(cfg)]
+    # Q fragments of both chains -> AGPRs (Q block in LDS at %[qb] + this wave's rows)
+    for t in range(NTQ):
+        seq.append(valu(f"v_add_u32 v{t}, %[qb], %[ka{t}]", [], [f"v{t}"]))
+    for c in range(2):
+        for t in range(NTQ):
+            d = cfg.Q(c, t)
+            seq.append(Ins(f"ds_read_b128 {rtxt('a', d, 4)}, v{t} offset:{c * 32 * D * 2}", "dsr", R([f"v{t}"]),
+                           rng("a", d, 4)))
+    # K(0) fragments: ring slots, then (D = 128) the NM registers as spare slots
+    kreg0 = lambda f: cfg.Kr(f) if f < cfg.ring else 64 + 4 * (f - cfg.ring)
+    for f in range(NKF):
+        seq.append(kfrag_read(cfg, f, 0, kreg0(f)))
+    # Sᵀ of tile 0 for both chains (no -m seed yet)
+    seq += qk_mfmas_zero(cfg, 0, kreg0) + qk_mfmas_zero(cfg, 1, kreg0)
+    # row max per chain -> m; the two lane halves hold the two key halves: xor-32 max
+    for c in range(2):
+        m = cfg.m(c)
+        regs = [cfg.S(c, kb, i) for kb in range(2) for i in range(16)]
+        seq.append(valu(f"v_max3_f32 v{m}, v{regs[0]}, v{regs[1]}, v{regs[2]}", [f"v{r}" for r in regs[:3]], [f"v{m}"]))
+        k = 3
+        while k + 1 < len(regs):
+            seq.append(valu(f"v_max3_f32 v{m}, v{m}, v{regs[k]}, v{regs[k + 1]}", [f"v{m}", f"v{regs[k]}", f"v{regs[k + 1]}"],
+                            [f"v{m}"]))
+            k += 2
+        if k < len(regs):
+            seq.append(valu(f"v_max_f32 v{m}, v{m}, v{regs[k]}", [f"v{m}", f"v{regs[k]}"], [f"v{m}"]))
+        t0, t1 = cfg.tmp(0), cfg.tmp(1)
+        seq.append(valu(f"v_mov_b32 v{t0}, v{m}", [f"v{m}"], [f"v{t0}"]))
+        seq.append(valu(f"v_mov_b32 v{t1}, v{m}", [f"v{m}"], [f"v{t1}"]))
+        seq.append(valu(f"v_permlane32_swap_b32 v{t0}, v{t1}", [f"v{t0}", f"v{t1}"], [f"v{t0}", f"v{t1}"]))
+        seq.append(valu(f"v_max_f32 v{m}, v{t0}, v{t1}", [f"v{t0}", f"v{t1}"], [f"v{m}"]))
+    # -m splats (the QKᵀ seeds) and s - m of tile 0
+    for c in range(2):
+        m, nm = cfg.m(c), cfg.NM(c)
+        seq.append(valu(f"v_sub_f32 v{nm}, 0, v{m}", [f"v{m}"], [f"v{nm}"]))
+        for i in range(1, 16):
+            seq.append(valu(f"v_mov_b32 v{nm + i}, v{nm}", [f"v{nm}"], [f"v{nm + i}"]))
+        for kb in range(2):
+            for i in range(16):
+                r = cfg.S(c, kb, i)
+                seq.append(valu(f"v_sub_f32 v{r}, v{r}, v{m}", [f"v{r}", f"v{m}"], [f"v{r}"]))
+    seq += softmax_part(cfg, 0, 0, False) + softmax_part(cfg, 0, 1, True) + softmax_part(cfg, 1, 0, False)
+    # V(0) fragments, O[B] = 0, PV of chain A (tile 0)
+    for i in range(cfg.NF):
+        seq += vfrag_reads(cfg, i, 0)
+    for b in range(cfg.NB):
+        for i in range(16):
+            r = cfg.O(1, b) + i
+            seq.append(valu(f"v_accvgpr_write_b32 a{r}, 0", [], [f"a{r}"]))
+    seq += pv_mfmas(cfg, 0, first=True)
+    # tile 1 -> slot 1, tile 2 loads, barrier, K(1) fragment prefetch
+    seq += staging_convert(cfg, 0, 1) + staging_convert(cfg, 1, 1)
+    seq += staging_loads(cfg, 0) + staging_loads(cfg, 1) + [goff_inc(cfg)]
+    seq += [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_barrier", "bar")]
+    seq += [kfrag_read(cfg, f, 1, cfg.Kr(f)) for f in range(min(cfg.ring, NKF))]
+    return seq
+
+
+def epilogue(cfg):
+    D = cfg.D
+    seq = [Ins("s_waitcnt vmcnt(0) lgkmcnt(0)", "wait")]
+    seq += softmax_part(cfg, 1, 1, True)
+    seq += pv_mfmas(cfg, 1)
+    # every wave is done with the tile slots before the O stage overwrites them
+    seq.append(Ins("s_barrier", "bar"))
+    for c in range(2):
+        for b in range(cfg.NB):
+            for g in range(4):
+                r = cfg.O(c, b) + 4 * g
+                off = (c * 32 * cfg.OST + 32 * b + 8 * g) * 4
+                seq.append(Ins(f"ds_write_b128 %[oa], {rtxt('a', r, 4)} offset:{off}", "dsw", R(rng("a", r, 4)), []))
+    for c in range(2):
+        seq.append(valu(f"v_mov_b32 %[om{c}], v{cfg.m(c)}", [f"v{cfg.m(c)}"], []))
+        seq.append(valu(f"v_mov_b32 %[ol{c}], v{cfg.l(c)}", [f"v{cfg.l(c)}"], []))
+    seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
+    return seq
+
+
+# ---------------------------------------------------------------------------------------
+# counted waits and hazard wait states
+# ---------------------------------------------------------------------------------------
+def regs_of(ins):
+    return {r for r, _ in ins.rd} | set(ins.wr)
+
+
+def insert_waits(seq, state):
+    """state: (lgkm list, vm list) of outstanding ops as frozensets of written regs"""
+    lg, vm = [list(state[0]), list(state[1])]
+    out = []
+    for ins in seq:
+        if ins.kind == "wait":
+            t = ins.text
+            if "lgkmcnt(" in t:
+                n = int(t.split("lgkmcnt(")[1].split(")")[0])
+                lg = lg[len(lg) - n:] if n < len(lg) else lg
+            if "vmcnt(" in t:
+                n = int(t.split("vmcnt(")[1].split(")")[0])
+                vm = vm[len(vm) - n:] if n < len(vm) else vm
+            out.append(ins)
+            continue
+        touched = regs_of(ins)
+        nl = nv = None
+        for idx, e in enumerate(lg):
+            if e & touched:
+                nl = len(lg) - idx - 1
+        for idx, e in enumerate(vm):
+            if e & touched:
+                nv = len(vm) - idx - 1
+        parts = []
+        if nv is not None:
+            nv = min(nv, 63)
+            parts.append(f"vmcnt({nv})")
+            vm = vm[len(vm) - nv:] if nv else []
+        if nl is not None:
+            nl = min(nl, 15)
+            parts.append(f"lgkmcnt({nl})")
+            lg = lg[len(lg) - nl:] if nl else []
+        if parts:
+            out.append(Ins("s_waitcnt " + " ".join(parts), "wait"))
+        out.append(ins)
+        if ins.kind in ("dsr", "dsw"):
+            lg.append(frozenset(ins.wr))
+        elif ins.kind == "vmem":
+            vm.append(frozenset(ins.wr))
+    return out, (tuple(lg), tuple(vm))
+
+
+MFMA_RESULT_WS = 12  # 8-pass XDL (32x32x16) result -> any non-chain reader or writer (gfx950)
+
+
+def hazard_need(prev, cur):
+    """wait states cur needs after prev (0 if none)"""
+    need = 0
+    pw = set(prev.wr)
+    if not pw:
+        return 0
+    if prev.kind == "mfma":
+        for r, role in cur.rd:
+            if r in pw:
+                if cur.kind == "mfma" and role == "C" and set(cur.wr) == pw:
+                    continue  # accumulate chain: back-to-back
+                need = max(need, MFMA_RESULT_WS)
+        if set(cur.wr) & pw and not (cur.kind == "mfma" and set(cur.wr) == pw):
+            need = max(need, MFMA_RESULT_WS)
+        return need
+    if prev.kind in ("valu", "exp"):
+        rd = {r for r, _ in cur.rd}
+        hit = rd & pw
+        if not hit:
+            return 0
+        if cur.kind == "mfma" or cur.perm:
+            need = max(need, 2)
+        if prev.trans and cur.kind in ("valu", "exp") and not cur.trans:
+            need = max(need, 1)
+        if prev.perm:
+            need = max(need, 2)
+        if "vcc" in hit and cur.kind == "salu":
+            need = max(need, 1)
+        return need
+    if prev.kind == "salu":
+        if {r for r, _ in cur.rd} & pw and cur.kind == "vmem":
+            return 1
+    return 0
+
+
+def fix_hazards(block, preds):
+    """insert s_nop into block so every consumer has its wait states after every producer,
+    with each predecessor tail in preds as possible history"""
+    out = []
+    for ins in block:
+        need = 0
+        for hist in preds:
+            h = hist + out
+            dist = 0
+            for prev in reversed(h):
+                if dist > 24:
+                    break
+                n = hazard_need(prev, ins)
+                if n > dist:
+                    need = max(need, n - dist)
+                dist += prev.ws()
+        while need > 0:
+            k = min(need, 16)
+            out.append(Ins(f"s_nop {k - 1}", "nop"))
+            need -= k
+        out.append(ins)
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# whole program
+# ---------------------------------------------------------------------------------------
+def build(cfg):
+    log = [f"D={cfg.D} {'bf16' if cfg.bf16 else 'fp16'}: {cfg.nvgpr} VGPRs + {cfg.nagpr} AGPRs in asm, "
+           f"LDS {cfg.lds_bytes} B"]
+    pro = prologue(cfg)
+    b1 = body(cfg, 1, log)
+    b0 = body(cfg, 0, log)
+    epi = epilogue(cfg)
+    empty = ((), ())
+    pro, st_p = insert_waits(pro, empty)
+    b1, st_1 = insert_waits(b1, st_p)
+    b0, st_0 = insert_waits(b0, st_1)
+    assert st_0 == st_p, "loop-carried wait state differs between the prologue exit and the loop back edge"
+    epi, _ = insert_waits(epi, ((), ()))  # starts with a full drain
+    loop_ctl1 = [Ins("s_sub_u32 %[cnt], %[cnt], 1", "salu", R(["s:cnt"]), ["s:cnt", "scc"]),
+                 Ins("s_cmp_eq_u32 %[cnt], 0", "salu", R(["s:cnt"]), ["scc"]),
+                 Ins("s_cbranch_scc1 FA2HS_EPI_%=", "branch", R(["scc"]))]
+    loop_ctl0 = [Ins("s_sub_u32 %[cnt], %[cnt], 1", "salu", R(["s:cnt"]), ["s:cnt", "scc"]),
+                 Ins("s_cmp_lg_u32 %[cnt], 0", "salu", R(["s:cnt"]), ["scc"]),
+                 Ins("s_cbranch_scc1 FA2HS_LOOP_%=", "branch", R(["scc"]))]
+    b1 = b1 + loop_ctl1
+    b0 = b0 + loop_ctl0
+    for _ in range(3):
+        pro = fix_hazards(pro, [[]])
+        b1 = fix_hazards(b1, [pro[-40:], b0[-40:]])
+        b0 = fix_hazards(b0, [b1[-40:]])
+        epi = fix_hazards(epi, [b1[-40:], b0[-40:]])
+    lines = [i.text for i in pro] + ["FA2HS_LOOP_%=:"] + [i.text for i in b1] + [i.text for i in b0] + \
+            ["FA2HS_EPI_%=:"] + [i.text for i in epi]
+    nm = sum(1 for i in b1 + b0 if i.kind == "mfma")
+    nv = sum(1 for i in b1 + b0 if i.kind in ("valu", "exp"))
+    nn = sum(int(i.text.split()[1]) + 1 for i in b1 + b0 if i.kind == "nop")
+    log.append(f"  loop (2 tiles): {nm} MFMA, {nv} VALU ({nv / nm:.2f} per MFMA), {nn} nop wait states, "
+               f"{len(b1) + len(b0)} instructions")
+    return lines, log
+
+
+def operands(cfg):
+    outs = ['[om0] "=&v"(hs_m0)', '[om1] "=&v"(hs_m1)', '[ol0] "=&v"(hs_l0)', '[ol1] "=&v"(hs_l1)',
+            '[flg] "=&s"(hs_flag)', '[cnt] "+s"(hs_cnt)', '[goff] "+s"(hs_goff)']
+    ins = [f'[ka{t}] "v"(hs_ka[{t}])' for t in range(cfg.NTQ)]
+    ins += [f'[va{b}_{k}] "v"(hs_va[{b}][{k}])' for b in range(cfg.NB) for k in range(2)]
+    ins += [f'[vo{c}] "v"(hs_vo[{c}])' for c in range(cfg.CPT)]
+    ins += ['[lo] "v"(hs_lo)', '[oa] "v"(hs_oa)', '[rsk] "s"(hs_rsk)', '[rsv] "s"(hs_rsv)', '[qb] "s"(hs_qb)']
+    clob = [f'"v{i}"' for i in range(cfg.nvgpr)] + [f'"a{i}"' for i in range(cfg.nagpr)] + ['"vcc"', '"scc"', '"memory"']
+    return outs, ins, clob
+
+
+def emit():
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = ["// Generated by cuda-flash-attention_amd/gen/gen_fwd_hs.py -- do not edit.",
+           "// Hand-scheduled forward tile loop of fa2_fwd_hs_kernel<D> (kernel_fa2_optimized_f16.cu).",
+           "#pragma once", ""]
+    logs = []
+    for D in (64, 128):
+        for bf16 in (False, True):
+            cfg = Cfg(D, bf16)
+            lines, log = build(cfg)
+            logs += log
+            tag = f"D{D}_{'BF16' if bf16 else 'F16'}"
+            out.append(f"#define FA2_HS_ASM_{tag} \\")
+            out += [f'    "{ln}\\n\\t" \\' for ln in lines]
+            out.append('    ""')
+            out.append("")
+        cfg = Cfg(D, False)
+        o, i, c = operands(cfg)
+        out.append(f"#define FA2_HS_OUTPUTS_D{D} " + ", ".join(o))
+        out.append(f"#define FA2_HS_INPUTS_D{D} " + ", ".join(i))
+        out.append(f"#define FA2_HS_CLOBBERS_D{D} " + ", ".join(c))
+        out.append(f"#define FA2_HS_LDS_D{D} {cfg.lds_bytes}")
+        out.append("")
+    out = ["// " + ln for ln in logs] + out
+    text = "\n".join(out) + "\n"
+    path = os.path.join(here, "..", "kernels", "fa2_fwd_hs.inc")
+    if "--check" in sys.argv:
+        cur = open(path).read() if os.path.exists(path) else ""
+        if cur != text:
+            print("fa2_fwd_hs.inc is stale: run gen/gen_fwd_hs.py")
+            sys.exit(1)
+        return
+    with open(path, "w") as f:
+        f.write(text)
+    print("\n".join(logs))
+
+
+if __name__ == "__main__":
+    emit()

@@ -822,6 +822,146 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
 #endif
 }
 
+#ifndef CUPY_INLINE_COMPILE
+// ---------------------------------------------------------------------------
+// Hand-scheduled forward (D = 64, 128; S % 64 == 0, S >= 128), r05.
+// ---------------------------------------------------------------------------
+// One workgroup = 4 waves = 256 query rows, one wave per SIMD with the whole register
+// file; each wave keeps 64 query rows as two 32-row chains and runs, per 64-key tile,
+// four MFMA phases with the other chain's softmax placed in their gaps (QKᵀ of A |
+// softmax of B, PV of B | softmax of A, QKᵀ of B | softmax of A, PV of A | softmax of
+// B).  The tile loop is the generated inline-asm block of fa2_fwd_hs.inc
+// (gen/gen_fwd_hs.py: register map, gap schedule, counted waits, hazard states); this
+// kernel stages the Q block and the first K/V tile, hands the asm its per-lane LDS
+// offsets, staging offsets and buffer descriptors, and finishes with the O rows the
+// asm leaves (unnormalised, fp32) in an LDS stage.  Same results as the reference's
+// flash_attention2_forward_kernel_fp16 (kernel_fa2_optimized_f16.cu:97-330): the m
+// reference point is the first tile's row max, every later tile's half-row sums are
+// checked against 2^13 (fp16 range of P), and a block where any was out of range (or
+// NaN) is recomputed by the robust compiler-scheduled loop below.
+}  // namespace fa2f16
+#include "fa2_fwd_hs.inc"
+namespace fa2f16 {
+
+template <int D>
+__global__ void __launch_bounds__(256, 1)
+fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                  float* __restrict__ O, float* __restrict__ LSE, int S) {
+    static_assert(D == 64 || D == 128, "hand-scheduled forward: D = 64 or 128");
+    constexpr int KT = 64, TB = KT * D;  // halves per tile image
+    constexpr int OST = D + 4;           // O stage row stride (floats), as in the generator
+    constexpr int LDSB = D == 64 ? FA2_HS_LDS_D64 : FA2_HS_LDS_D128;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[LDSB / 2];
+    __shared__ float invl[256];
+
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nqb = (S + 255) / 256;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = bid / nqb, qb = bid - bh * nqb;
+    const long base = (long)bh * S * D;
+    const int qrow0 = qb * 256;
+
+    // Q block (256 rows, scaled by log2(e)/sqrt(D)) -> LDS [4TB, 8TB) halves; K(0), V(0)
+    // -> slot 0 of the K and V rings ([0, TB) and [2TB, 3TB))
+    TileStager<D, KT, 256> ks, vs;
+    ks.init(K + base, S, tid);
+    vs.init(V + base, S, tid);
+    {
+        TileStager<D, 256, 256> qst;
+        qst.init(Q + base, S, tid);
+        qst.load(qrow0);
+        ks.load(0);
+        vs.load(0);
+        qst.store(smem + 4 * TB, FA2_LOG2E / __builtin_sqrtf((float)D), tid);
+        ks.store(smem, 1.f, tid);
+        vs.store(smem + 2 * TB, 1.f, tid);
+    }
+    __syncthreads();
+
+    FragOffsets<D> fo;
+    fo.init(lane);
+    int hs_ka[D / 16], hs_va[D / 32][2], hs_vo[D / 32];
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) hs_ka[t] = fo.row[t] * 2;
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b) {
+        hs_va[b][0] = fo.tr[b][0] * 2;
+        hs_va[b][1] = fo.tr[b][1] * 2;
+    }
+#pragma unroll
+    for (int c = 0; c < D / 32; ++c) hs_vo[c] = ks.voff[c];
+    const int hs_lo = ks.loff[0] * 2;
+    const int hs_oa = ((wave * 64 + r) * OST + 4 * h) * 4;
+    const __amdgpu_buffer_rsrc_t hs_rsk = ks.rs, hs_rsv = vs.rs;
+    const int hs_qb = __builtin_amdgcn_readfirstlane(4 * TB * 2 + wave * 64 * D * 2);
+    int hs_cnt = __builtin_amdgcn_readfirstlane(S / KT - 1);
+    int hs_goff = __builtin_amdgcn_readfirstlane(KT * D * 4);
+    float hs_m0, hs_m1, hs_l0, hs_l1;
+    unsigned long long hs_flag;
+    if constexpr (D == 64) {
+#ifdef FA2_TILE_BF16
+        asm volatile(FA2_HS_ASM_D64_BF16 : FA2_HS_OUTPUTS_D64 : FA2_HS_INPUTS_D64 : FA2_HS_CLOBBERS_D64);
+#else
+        asm volatile(FA2_HS_ASM_D64_F16 : FA2_HS_OUTPUTS_D64 : FA2_HS_INPUTS_D64 : FA2_HS_CLOBBERS_D64);
+#endif
+    } else {
+#ifdef FA2_TILE_BF16
+        asm volatile(FA2_HS_ASM_D128_BF16 : FA2_HS_OUTPUTS_D128 : FA2_HS_INPUTS_D128 : FA2_HS_CLOBBERS_D128);
+#else
+        asm volatile(FA2_HS_ASM_D128_F16 : FA2_HS_OUTPUTS_D128 : FA2_HS_INPUTS_D128 : FA2_HS_CLOBBERS_D128);
+#endif
+    }
+
+    if (!__syncthreads_or(hs_flag != 0)) {
+        // O rows [wave*64 + c*32 + q][OST] (unnormalised) are in the stage; l is per lane
+        // half: the xor-32 sum is the row's total
+        const float lt0 = xor32_sum(hs_l0), lt1 = xor32_sum(hs_l1);
+        if (h == 0) {
+            invl[wave * 64 + r] = 1.f / lt0;
+            invl[wave * 64 + 32 + r] = 1.f / lt1;
+            const int q0 = qrow0 + wave * 64 + r;
+            if (q0 < S) LSE[(long)bh * S + q0] = hs_m0 * FA2_LN2 + __logf(lt0);
+            if (q0 + 32 < S) LSE[(long)bh * S + q0 + 32] = hs_m1 * FA2_LN2 + __logf(lt1);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // whole rows: D/4 lanes per row, 16-B pieces
+        constexpr int LPR = D / 4, RPI = 64 / LPR;
+        const float* os = reinterpret_cast<const float*>(smem);
+#pragma unroll 4
+        for (int rr = 0; rr < 64; rr += RPI) {
+            const int row = wave * 64 + rr + lane / LPR, c4 = (lane % LPR) * 4;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(os + row * OST + c4) * invl[row];
+            if (qrow0 + row < S) *reinterpret_cast<f32x4*>(O + base + (long)(qrow0 + row) * D + c4) = v;
+        }
+        return;
+    }
+    // Robust path (a late score spike somewhere in the block): both chains of every wave
+    // recomputed with the rescaling loop (first tile sets m, later tiles move it when
+    // their sums leave range), one chain at a time.
+#pragma unroll 1
+    for (int c = 0; c < 2; ++c) {
+        FwdState<D> st[1];
+        const int q = qrow0 + wave * 64 + c * 32 + r;
+        fwd_init<D>(st[0], Q, base, q, S, h);
+        const int ntiles = (S + KT - 1) / KT;
+#pragma unroll 1
+        for (int j = 0; j < ntiles; ++j) {
+            ks.load(j * KT);
+            vs.load(j * KT);
+            __syncthreads();
+            ks.store(smem, 1.f, tid);
+            vs.store(smem + TB, 1.f, tid);
+            __syncthreads();
+            f32x16 sacc[1][2];
+            fwd_qk<D, 1, 2, true>(sacc, st, smem, fo);
+            fwd_softmax_pv<D, 1, false, 2, true>(st, sacc, smem + TB, fo, j * KT, S, h, j == 0);
+        }
+        fwd_store<D>(st[0], O, LSE, base, (long)bh * S, q, S, h);
+    }
+}
+#endif  // CUPY_INLINE_COMPILE
+
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
 // block 256, test_flash_attention2.py:278-281 / kernel_fa2_optimized_f16.cu:401),
 // fp16 tiles on MFMA like the library kernel.  A workgroup owns 32 query rows;
@@ -910,8 +1050,28 @@ static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v,
 }
 
 template <int D>
+static hipError_t fwd_hs_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
+                                hipStream_t stream) {
+    const long grid = (long)bh * ((S + 255) / 256);
+    if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_hs_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, o, lse, S);
+    return hipGetLastError();
+}
+
+template <int D>
 static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
                                    hipStream_t stream) {
+    if constexpr (D == 64 || D == 128) {
+        // hand-scheduled kernel (r05): full 64-key tiles only, and a grid of at least one
+        // 256-row workgroup per CU (smaller grids keep the key-split plans below).
+        // FWD_HS (tests and tools): 1 forces it (an error where it cannot serve), 0 disables it
+        const int hs = tune_knob("FWD_HS", -1);
+        const bool fits = S % 64 == 0 && S >= 128;
+        if (hs == 1 && !fits) return hipErrorInvalidValue;
+        const bool forced_other = tune_knob("FWD_WAVES", 0) || tune_knob("FWD_KS", 0) || tune_knob("FWD_NKB", 0);
+        if (fits && (hs == 1 || (hs < 0 && !forced_other && (long)bh * ((S + 255) / 256) >= cu_count())))
+            return fwd_hs_launch<D>(q, k, v, o, lse, bh, S, stream);
+    }
     // 8 waves (2 per SIMD) where the registers allow it; D = 128 runs 4 waves of
     // ~400 VGPRs (8 would spill and exceed the LDS budget with the Q stages)
     // (MQ = 2, two 32-row query groups per wave at 4 waves / 1 per SIMD, measured

@@ -288,3 +288,22 @@ def test_bench_traffic_only_from_a_profile_of_the_loaded_build(tmp_path):
     summ["_meta"].pop("build_id")
     p.write_text(json.dumps(summ))
     assert bench.traffic_from_profile("dkdv", 64, 2048, 64, bid, str(p)) is None
+
+
+def test_no_float_atomics_on_any_fa2_path():
+    """dQ is written once on every face and precision (the reference adds it with
+    atomicAdd, f-attn2-backward.cu:298 / f-attn2-backward_f16.cu:289): no kernel source
+    of the library issues a float atomic, so every output is bitwise repeatable."""
+    kdir = os.path.join(os.path.dirname(fa2amd.LIB_PATH), "..", "kernels")
+    pat = re.compile(r"\batomicAdd\s*\(|__hip_atomic_fetch_add|unsafeAtomicAdd|global_atomic_add")
+    for name in sorted(os.listdir(kdir)):
+        if name.endswith((".cu", ".cuh", ".inc")):
+            with open(os.path.join(kdir, name)) as f:
+                assert not pat.search(f.read()), name
+
+
+def test_generated_forward_loop_is_current():
+    """kernels/fa2_fwd_hs.inc is what gen/gen_fwd_hs.py writes from its current source"""
+    gen = os.path.join(os.path.dirname(fa2amd.LIB_PATH), "..", "gen", "gen_fwd_hs.py")
+    r = subprocess.run(["python3", gen, "--check"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
