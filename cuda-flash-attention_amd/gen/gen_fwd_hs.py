@@ -266,7 +266,7 @@ def softmax_part(cfg, c, kb, final):
         out.append(valu(f"v_add_f32 v{ts}, v{T[0]}, v{T[2]}", [f"v{T[0]}", f"v{T[2]}"], [f"v{ts}"]))
         out.append(valu(f"v_add_f32 v{cfg.l(c)}, v{cfg.l(c)}, v{ts}", [f"v{cfg.l(c)}", f"v{ts}"], [f"v{cfg.l(c)}"]))
         # NaN or a half-row sum above 2^13 -> the block is recomputed by the robust path
-        out.append(valu(f"v_cmp_nle_f32 vcc, {SUM_MAX_BITS:#x}, v{ts}", [f"v{ts}"], ["vcc"]))
+        out.append(valu(f"v_cmp_nge_f32 vcc, {SUM_MAX_BITS:#x}, v{ts}", [f"v{ts}"], ["vcc"]))  # !(2^13 >= ts)
         out.append(Ins("s_or_b64 %[flg], %[flg], vcc", "salu", R(["vcc", "s:flg"]), ["s:flg"]))
     return out
 

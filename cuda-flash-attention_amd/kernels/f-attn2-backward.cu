@@ -11,9 +11,9 @@
 // no atomics and needs no pre-zeroing: a workgroup in the dQ ROLE owns 32 query
 // rows and walks all keys (recomputing S and dP for them), so every dQ element is
 // summed in one fixed order inside one workgroup and written once.  Results are
-// bitwise reproducible and no cross-XCD read-modify-write of dQ exists (r03's
-// zero-then-atomics design lost one key block's dQ on a driver box: the per-XCD L2s
-// are not coherent with each other, MI355X_MICROARCH §XCD placement).
+// bitwise reproducible and no cross-workgroup read-modify-write of dQ exists.  (r03's
+// zero-then-atomics design lost one key block's dQ once on a driver box; DESIGN.md §3
+// "Exact-fp32 path" records what the evidence does and does not establish about why.)
 //
 // Roles (both on v_mfma_f32_32x32x2_f32, exact fp32 products, fp32 accumulation):
 //   dK/dV role (4 GEMMs): 32 keys per workgroup; the four waves split the query
