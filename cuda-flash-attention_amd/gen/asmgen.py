@@ -1,0 +1,218 @@
+"""Shared machinery of the inline-asm generators (gen_fwd_hs.py, gen_bwd_*.py), gfx950.
+
+  Ins              one instruction: text, class, registers read (with MFMA operand role) and
+                   written, issue cost, placement window (earliest / deadline MFMA gap)
+  schedule_phase   list scheduler: the filler streams of a phase into its MFMA gaps, with a
+                   per-gap issue budget and at most `exp_per_gap` v_exp per gap
+  insert_waits     exact counted s_waitcnt lgkmcnt / vmcnt before every consumer of an
+                   outstanding ds_read / buffer_load (in-order retirement)
+  fix_hazards      s_nop wait states from the gfx950 rules: MFMA result -> any other reader
+                   or writer (8-pass 32x32x16: 12 states, 4-pass 16x16x32: 8), VALU -> MFMA
+                   operand 2, transcendental -> VALU 1, VALU -> permlane 2, permlane -> VALU 2
+"""
+
+
+class Ins:
+    """One instruction: text, class, registers read (with MFMA operand role) and written."""
+
+    __slots__ = ("text", "kind", "rd", "wr", "cost", "earliest", "deadline", "trans", "perm", "tag")
+
+    def __init__(self, text, kind, rd=(), wr=(), cost=None, earliest=0, deadline=None):
+        self.text = text
+        self.kind = kind  # mfma valu exp dsr dsw vmem salu wait nop bar label branch
+        self.rd = list(rd)  # list of (reg, role)
+        self.wr = list(wr)
+        self.earliest = earliest
+        self.deadline = deadline
+        self.trans = kind == "exp"
+        self.perm = text.startswith("v_permlane")
+        self.tag = ""
+        if cost is None:
+            cost = {"mfma": 8, "exp": 8, "valu": 4, "dsr": 4, "dsw": 8, "vmem": 4, "salu": 2, "wait": 0,
+                    "nop": 4, "bar": 4, "label": 0, "branch": 4}[kind]
+        self.cost = cost
+
+    def ws(self):
+        """wait states this instruction provides to a later hazard consumer"""
+        if self.kind == "label":
+            return 0
+        if self.kind == "nop":
+            return int(self.text.split()[1]) + 1
+        return 1
+
+
+def tagged(tag, seq):
+    for i in seq:
+        i.tag = tag
+    return seq
+
+
+def rng(p, base, n):
+    return [f"{p}{base + i}" for i in range(n)]
+
+
+def rtxt(p, base, n):
+    return f"{p}{base}" if n == 1 else f"{p}[{base}:{base + n - 1}]"
+
+
+def R(regs, role="x"):
+    return [(r, role) for r in regs]
+
+
+def valu(text, rd, wr, kind="valu"):
+    return Ins(text, kind, R(rd), wr)
+
+
+def schedule_phase(cfg, mfmas, streams, name, log):
+    """cfg: any object with exp_per_gap"""
+    nM = len(mfmas)
+    streams = [s for s in streams if s]
+    pos = [0] * len(streams)
+    tot = [max(1, sum(i.cost for i in s)) for s in streams]
+    done = [0] * len(streams)
+    total = sum(sum(i.cost for i in s) for s in streams)
+    cap = max(24, -(-total // max(1, nM)))
+    out = []
+    for g in range(nM + 1):
+        used = 0
+        nexp = 0
+        while True:
+            cands = [k for k, s in enumerate(streams) if pos[k] < len(s) and s[pos[k]].earliest <= g]
+            if not cands:
+                break
+            forced = [k for k in cands if streams[k][pos[k]].deadline is not None and streams[k][pos[k]].deadline <= g]
+            if forced:
+                k = min(forced, key=lambda k: streams[k][pos[k]].deadline)
+            else:
+                if g < nM and used >= cap:
+                    break
+                ok = [k for k in cands if g == nM or not (streams[k][pos[k]].kind == "exp" and nexp >= cfg.exp_per_gap)]
+                if not ok:
+                    break
+                k = min(ok, key=lambda k: (done[k] / tot[k], k))
+            ins = streams[k][pos[k]]
+            pos[k] += 1
+            done[k] += ins.cost
+            used += ins.cost
+            nexp += ins.kind == "exp"
+            out.append(ins)
+        if g < nM:
+            out.append(mfmas[g])
+    for k, s in enumerate(streams):
+        assert pos[k] == len(s), f"{name}: stream {k} not drained"
+    nexp = sum(1 for s in streams for i in s if i.kind == "exp")
+    nfill = sum(len(s) for s in streams)
+    log.append(f"  {name:4s}: {nM:2d} MFMA, {nfill:3d} fillers ({nexp} exp), filler issue {total:4d} cyc, "
+               f"cap/gap {cap}, est. {max(32 * nM, total + 8 * nM)} cyc")
+    return out
+
+
+def regs_of(ins):
+    return {r for r, _ in ins.rd} | set(ins.wr)
+
+
+def insert_waits(seq, state):
+    """state: (lgkm list, vm list) of outstanding ops as frozensets of written regs"""
+    lg, vm = [list(state[0]), list(state[1])]
+    out = []
+    for ins in seq:
+        if ins.kind == "wait":
+            t = ins.text
+            if "lgkmcnt(" in t:
+                n = int(t.split("lgkmcnt(")[1].split(")")[0])
+                lg = lg[len(lg) - n:] if n < len(lg) else lg
+            if "vmcnt(" in t:
+                n = int(t.split("vmcnt(")[1].split(")")[0])
+                vm = vm[len(vm) - n:] if n < len(vm) else vm
+            out.append(ins)
+            continue
+        touched = regs_of(ins)
+        nl = nv = None
+        for idx, e in enumerate(lg):
+            if e & touched:
+                nl = len(lg) - idx - 1
+        for idx, e in enumerate(vm):
+            if e & touched:
+                nv = len(vm) - idx - 1
+        parts = []
+        if nv is not None:
+            nv = min(nv, 63)
+            parts.append(f"vmcnt({nv})")
+            vm = vm[len(vm) - nv:] if nv else []
+        if nl is not None:
+            nl = min(nl, 15)
+            parts.append(f"lgkmcnt({nl})")
+            lg = lg[len(lg) - nl:] if nl else []
+        if parts:
+            out.append(Ins("s_waitcnt " + " ".join(parts), "wait"))
+        out.append(ins)
+        if ins.kind in ("dsr", "dsw"):
+            lg.append(frozenset(ins.wr))
+        elif ins.kind == "vmem":
+            vm.append(frozenset(ins.wr))
+    return out, (tuple(lg), tuple(vm))
+
+
+def mfma_result_ws(ins):
+    """wait states after an MFMA before another instruction may read or write its result
+    (gfx950: passes + 4; the chained accumulate into the same registers needs none)"""
+    return 8 if "16x16x32" in ins.text else 12
+
+
+def hazard_need(prev, cur):
+    """wait states cur needs after prev (0 if none)"""
+    need = 0
+    pw = set(prev.wr)
+    if not pw:
+        return 0
+    if prev.kind == "mfma":
+        for r, role in cur.rd:
+            if r in pw:
+                if cur.kind == "mfma" and role == "C" and set(cur.wr) == pw:
+                    continue  # accumulate chain: back-to-back
+                need = max(need, mfma_result_ws(prev))
+        if set(cur.wr) & pw and not (cur.kind == "mfma" and set(cur.wr) == pw):
+            need = max(need, mfma_result_ws(prev))
+        return need
+    if prev.kind in ("valu", "exp"):
+        rd = {r for r, _ in cur.rd}
+        hit = rd & pw
+        if not hit:
+            return 0
+        if cur.kind == "mfma" or cur.perm:
+            need = max(need, 2)
+        if prev.trans and cur.kind in ("valu", "exp") and not cur.trans:
+            need = max(need, 1)
+        if prev.perm:
+            need = max(need, 2)
+        if "vcc" in hit and cur.kind == "salu":
+            need = max(need, 1)
+        return need
+    if prev.kind == "salu":
+        if {r for r, _ in cur.rd} & pw and cur.kind == "vmem":
+            return 1
+    return 0
+
+
+def fix_hazards(block, preds):
+    """insert s_nop into block so every consumer has its wait states after every producer,
+    with each predecessor tail in preds as possible history"""
+    out = []
+    for ins in block:
+        need = 0
+        for hist in preds:
+            h = hist + out
+            dist = 0
+            for prev in reversed(h):
+                if dist > 24:
+                    break
+                n = hazard_need(prev, ins)
+                if n > dist:
+                    need = max(need, n - dist)
+                dist += prev.ws()
+        while need > 0:
+            k = min(need, 16)
+            out.append(Ins(f"s_nop {k - 1}", "nop"))
+            need -= k
+        out.append(ins)
+    return out

@@ -46,53 +46,13 @@ Usage: python3 gen_fwd_hs.py [--check]   (--check: verify the .inc is up to date
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from asmgen import Ins, R, fix_hazards, insert_waits, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402
+
 KT = 64  # keys per tile
 NWAVE = 4
 ROWS = 64 * NWAVE  # query rows per workgroup
 SUM_MAX_BITS = 0x46000000  # 8192.0f: half-row tile-sum guard (FA2_TILE_SUM_MAX)
-
-
-# ---------------------------------------------------------------------------------------
-# instructions
-# ---------------------------------------------------------------------------------------
-class Ins:
-    """One instruction: text, class, registers read (with MFMA operand role) and written."""
-
-    __slots__ = ("text", "kind", "rd", "wr", "cost", "earliest", "deadline", "trans", "perm")
-
-    def __init__(self, text, kind, rd=(), wr=(), cost=None, earliest=0, deadline=None):
-        self.text = text
-        self.kind = kind  # mfma valu exp dsr dsw vmem salu wait nop bar label branch
-        self.rd = list(rd)  # list of (reg, role)
-        self.wr = list(wr)
-        self.earliest = earliest
-        self.deadline = deadline
-        self.trans = kind == "exp"
-        self.perm = text.startswith("v_permlane")
-        if cost is None:
-            cost = {"mfma": 8, "exp": 8, "valu": 4, "dsr": 4, "dsw": 8, "vmem": 4, "salu": 2, "wait": 0,
-                    "nop": 4, "bar": 4, "label": 0, "branch": 4}[kind]
-        self.cost = cost
-
-    def ws(self):
-        """wait states this instruction provides to a later hazard consumer"""
-        if self.kind == "label":
-            return 0
-        if self.kind == "nop":
-            return int(self.text.split()[1]) + 1
-        return 1
-
-
-def rng(p, base, n):
-    return [f"{p}{base + i}" for i in range(n)]
-
-
-def rtxt(p, base, n):
-    return f"{p}{base}" if n == 1 else f"{p}[{base}:{base + n - 1}]"
-
-
-def R(regs, role="x"):
-    return [(r, role) for r in regs]
 
 
 # ---------------------------------------------------------------------------------------
@@ -185,26 +145,22 @@ def mfma(cfg, dst, a, b, c, c_is_zero=False):
     return Ins(text, "mfma", rd, rng(dst[0], dst[1], 16))
 
 
-def valu(text, rd, wr, kind="valu"):
-    return Ins(text, kind, R(rd), wr)
-
-
 def kfrag_read(cfg, f, slot, dst):
     kb, t = f // cfg.NTQ, f % cfg.NTQ
     off = cfg.koff(slot) + kb * 32 * cfg.D * 2
-    return Ins(f"ds_read_b128 {rtxt('v', dst, 4)}, %[ka{t}] offset:{off}", "dsr", [], rng("v", dst, 4))
+    return tagged("lds", [Ins(f"ds_read_b128 {rtxt('v', dst, 4)}, %[ka{t}] offset:{off}", "dsr", [], rng("v", dst, 4))])[0]
 
 
 def vfrag_reads(cfg, i, slot, earliest=0):
     b, off = cfg.vfrag_addr(i)
     off += cfg.voff(slot)
     d = cfg.Vf(i)
-    return [
+    return tagged("lds", [
         Ins(f"ds_read_b64_tr_b16 {rtxt('a', d, 2)}, %[va{b}_0] offset:{off}", "dsr", [], rng("a", d, 2),
             earliest=earliest),
         Ins(f"ds_read_b64_tr_b16 {rtxt('a', d + 2, 2)}, %[va{b}_1] offset:{off}", "dsr", [], rng("a", d + 2, 2),
             earliest=earliest),
-    ]
+    ])
 
 
 def qk_mfmas(cfg, c, kreg):
@@ -258,6 +214,7 @@ def softmax_part(cfg, c, kb, final):
         for ii in range(4):
             d, a, b = S(8 * s + ii), S(8 * s + 2 * ii), S(8 * s + 2 * ii + 1)
             out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
+    tagged("sm", out)
     if final:
         T = [cfg.T(c, k) for k in range(4)]
         ts = cfg.ts(c)
@@ -268,6 +225,8 @@ def softmax_part(cfg, c, kb, final):
         # NaN or a half-row sum above 2^13 -> the block is recomputed by the robust path
         out.append(valu(f"v_cmp_nge_f32 vcc, {SUM_MAX_BITS:#x}, v{ts}", [f"v{ts}"], ["vcc"]))  # !(2^13 >= ts)
         out.append(Ins("s_or_b64 %[flg], %[flg], vcc", "salu", R(["vcc", "s:flg"]), ["s:flg"]))
+        out[-6:-1] = tagged("sm", out[-6:-1])
+        out[-1].tag = "flag"
     return out
 
 
@@ -280,11 +239,11 @@ def staging_loads(cfg, tensor):
             off = f" offset:{16 * h}" if h else ""
             out.append(Ins(f"buffer_load_dwordx4 {rtxt('v', base + 4 * h, 4)}, %[vo{cc}], {rs}, %[goff] offen{off}",
                            "vmem", R(["s:goff"]), rng("v", base + 4 * h, 4)))
-    return out
+    return tagged("stg", out)
 
 
 def goff_inc(cfg):
-    return Ins(f"s_add_u32 %[goff], %[goff], {KT * cfg.D * 4}", "salu", R(["s:goff"]), ["s:goff", "scc"])
+    return tagged("stg", [Ins(f"s_add_u32 %[goff], %[goff], {KT * cfg.D * 4}", "salu", R(["s:goff"]), ["s:goff", "scc"])])[0]
 
 
 def staging_convert(cfg, tensor, slot):
@@ -298,53 +257,7 @@ def staging_convert(cfg, tensor, slot):
             out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
         off = toff + cc * rows_per_chunk_step * cfg.D * 2
         out.append(Ins(f"ds_write_b128 %[lo], {rtxt('v', base, 4)} offset:{off}", "dsw", R(rng("v", base, 4)), []))
-    return out
-
-
-# ---------------------------------------------------------------------------------------
-# list scheduler: MFMA gaps <- filler streams
-# ---------------------------------------------------------------------------------------
-def schedule_phase(cfg, mfmas, streams, name, log):
-    nM = len(mfmas)
-    streams = [s for s in streams if s]
-    pos = [0] * len(streams)
-    tot = [max(1, sum(i.cost for i in s)) for s in streams]
-    done = [0] * len(streams)
-    total = sum(sum(i.cost for i in s) for s in streams)
-    cap = max(24, -(-total // max(1, nM)))
-    out = []
-    for g in range(nM + 1):
-        used = 0
-        nexp = 0
-        while True:
-            cands = [k for k, s in enumerate(streams) if pos[k] < len(s) and s[pos[k]].earliest <= g]
-            if not cands:
-                break
-            forced = [k for k in cands if streams[k][pos[k]].deadline is not None and streams[k][pos[k]].deadline <= g]
-            if forced:
-                k = min(forced, key=lambda k: streams[k][pos[k]].deadline)
-            else:
-                if g < nM and used >= cap:
-                    break
-                ok = [k for k in cands if g == nM or not (streams[k][pos[k]].kind == "exp" and nexp >= cfg.exp_per_gap)]
-                if not ok:
-                    break
-                k = min(ok, key=lambda k: (done[k] / tot[k], k))
-            ins = streams[k][pos[k]]
-            pos[k] += 1
-            done[k] += ins.cost
-            used += ins.cost
-            nexp += ins.kind == "exp"
-            out.append(ins)
-        if g < nM:
-            out.append(mfmas[g])
-    for k, s in enumerate(streams):
-        assert pos[k] == len(s), f"{name}: stream {k} not drained"
-    nexp = sum(1 for s in streams for i in s if i.kind == "exp")
-    nfill = sum(len(s) for s in streams)
-    log.append(f"  {name:4s}: {nM:2d} MFMA, {nfill:3d} fillers ({nexp} exp), filler issue {total:4d} cyc, "
-               f"cap/gap {cap}, est. {max(32 * nM, total + 8 * nM)} cyc")
-    return out
+    return tagged("stg", out)
 
 
 # ---------------------------------------------------------------------------------------
@@ -484,131 +397,46 @@ def epilogue(cfg):
 
 
 # ---------------------------------------------------------------------------------------
-# counted waits and hazard wait states
+# whole program
 # ---------------------------------------------------------------------------------------
-def regs_of(ins):
-    return {r for r, _ in ins.rd} | set(ins.wr)
+ABL = set()  # timing-only ablations (gen_fwd_hs.py --abl a,b --out file): results are invalid
 
 
-def insert_waits(seq, state):
-    """state: (lgkm list, vm list) of outstanding ops as frozensets of written regs"""
-    lg, vm = [list(state[0]), list(state[1])]
+def ablate(seq):
+    """drop the loop-body instructions an ablation names (never in the product .inc)"""
+    if not ABL:
+        return seq
+    drop = set()
+    if "nobar" in ABL:
+        drop.add("bar")
+    if "nostage" in ABL:
+        drop.add("stg")
+    if "nolds" in ABL:
+        drop.add("lds")
+    if "nosm" in ABL:
+        drop.add("sm")
     out = []
-    for ins in seq:
-        if ins.kind == "wait":
-            t = ins.text
-            if "lgkmcnt(" in t:
-                n = int(t.split("lgkmcnt(")[1].split(")")[0])
-                lg = lg[len(lg) - n:] if n < len(lg) else lg
-            if "vmcnt(" in t:
-                n = int(t.split("vmcnt(")[1].split(")")[0])
-                vm = vm[len(vm) - n:] if n < len(vm) else vm
-            out.append(ins)
+    for i in seq:
+        if i.tag == "flag" or i.tag in drop or (i.kind == "bar" and "bar" in drop):
             continue
-        touched = regs_of(ins)
-        nl = nv = None
-        for idx, e in enumerate(lg):
-            if e & touched:
-                nl = len(lg) - idx - 1
-        for idx, e in enumerate(vm):
-            if e & touched:
-                nv = len(vm) - idx - 1
-        parts = []
-        if nv is not None:
-            nv = min(nv, 63)
-            parts.append(f"vmcnt({nv})")
-            vm = vm[len(vm) - nv:] if nv else []
-        if nl is not None:
-            nl = min(nl, 15)
-            parts.append(f"lgkmcnt({nl})")
-            lg = lg[len(lg) - nl:] if nl else []
-        if parts:
-            out.append(Ins("s_waitcnt " + " ".join(parts), "wait"))
-        out.append(ins)
-        if ins.kind in ("dsr", "dsw"):
-            lg.append(frozenset(ins.wr))
-        elif ins.kind == "vmem":
-            vm.append(frozenset(ins.wr))
-    return out, (tuple(lg), tuple(vm))
-
-
-MFMA_RESULT_WS = 12  # 8-pass XDL (32x32x16) result -> any non-chain reader or writer (gfx950)
-
-
-def hazard_need(prev, cur):
-    """wait states cur needs after prev (0 if none)"""
-    need = 0
-    pw = set(prev.wr)
-    if not pw:
-        return 0
-    if prev.kind == "mfma":
-        for r, role in cur.rd:
-            if r in pw:
-                if cur.kind == "mfma" and role == "C" and set(cur.wr) == pw:
-                    continue  # accumulate chain: back-to-back
-                need = max(need, MFMA_RESULT_WS)
-        if set(cur.wr) & pw and not (cur.kind == "mfma" and set(cur.wr) == pw):
-            need = max(need, MFMA_RESULT_WS)
-        return need
-    if prev.kind in ("valu", "exp"):
-        rd = {r for r, _ in cur.rd}
-        hit = rd & pw
-        if not hit:
-            return 0
-        if cur.kind == "mfma" or cur.perm:
-            need = max(need, 2)
-        if prev.trans and cur.kind in ("valu", "exp") and not cur.trans:
-            need = max(need, 1)
-        if prev.perm:
-            need = max(need, 2)
-        if "vcc" in hit and cur.kind == "salu":
-            need = max(need, 1)
-        return need
-    if prev.kind == "salu":
-        if {r for r, _ in cur.rd} & pw and cur.kind == "vmem":
-            return 1
-    return 0
-
-
-def fix_hazards(block, preds):
-    """insert s_nop into block so every consumer has its wait states after every producer,
-    with each predecessor tail in preds as possible history"""
-    out = []
-    for ins in block:
-        need = 0
-        for hist in preds:
-            h = hist + out
-            dist = 0
-            for prev in reversed(h):
-                if dist > 24:
-                    break
-                n = hazard_need(prev, ins)
-                if n > dist:
-                    need = max(need, n - dist)
-                dist += prev.ws()
-        while need > 0:
-            k = min(need, 16)
-            out.append(Ins(f"s_nop {k - 1}", "nop"))
-            need -= k
-        out.append(ins)
+        if "noexp" in ABL and i.kind == "exp":
+            continue
+        out.append(i)
     return out
 
 
-# ---------------------------------------------------------------------------------------
-# whole program
-# ---------------------------------------------------------------------------------------
 def build(cfg):
     log = [f"D={cfg.D} {'bf16' if cfg.bf16 else 'fp16'}: {cfg.nvgpr} VGPRs + {cfg.nagpr} AGPRs in asm, "
            f"LDS {cfg.lds_bytes} B"]
     pro = prologue(cfg)
-    b1 = body(cfg, 1, log)
-    b0 = body(cfg, 0, log)
+    b1 = ablate(body(cfg, 1, log))
+    b0 = ablate(body(cfg, 0, log))
     epi = epilogue(cfg)
     empty = ((), ())
     pro, st_p = insert_waits(pro, empty)
     b1, st_1 = insert_waits(b1, st_p)
     b0, st_0 = insert_waits(b0, st_1)
-    assert st_0 == st_p, "loop-carried wait state differs between the prologue exit and the loop back edge"
+    assert ABL or st_0 == st_p, "loop-carried wait state differs between the prologue exit and the loop back edge"
     epi, _ = insert_waits(epi, ((), ()))  # starts with a full drain
     loop_ctl1 = [Ins("s_sub_u32 %[cnt], %[cnt], 1", "salu", R(["s:cnt"]), ["s:cnt", "scc"]),
                  Ins("s_cmp_eq_u32 %[cnt], 0", "salu", R(["s:cnt"]), ["scc"]),
@@ -670,6 +498,8 @@ def emit():
     out = ["// " + ln for ln in logs] + out
     text = "\n".join(out) + "\n"
     path = os.path.join(here, "..", "kernels", "fa2_fwd_hs.inc")
+    if "--out" in sys.argv:
+        path = sys.argv[sys.argv.index("--out") + 1]
     if "--check" in sys.argv:
         cur = open(path).read() if os.path.exists(path) else ""
         if cur != text:
@@ -682,4 +512,7 @@ def emit():
 
 
 if __name__ == "__main__":
+    if "--abl" in sys.argv:
+        ABL.update(sys.argv[sys.argv.index("--abl") + 1].split(","))
+        assert "--out" in sys.argv, "ablation builds write elsewhere (--out): never the product .inc"
     emit()

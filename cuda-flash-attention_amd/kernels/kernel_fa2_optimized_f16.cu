@@ -840,7 +840,10 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
 // checked against 2^13 (fp16 range of P), and a block where any was out of range (or
 // NaN) is recomputed by the robust compiler-scheduled loop below.
 }  // namespace fa2f16
-#include "fa2_fwd_hs.inc"
+#ifndef FA2_HS_INC
+#define FA2_HS_INC "fa2_fwd_hs.inc"  // (timing-only ablation builds name another, tools/r05_hs_abl.sh)
+#endif
+#include FA2_HS_INC
 namespace fa2f16 {
 
 template <int D>
