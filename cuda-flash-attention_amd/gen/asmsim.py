@@ -60,6 +60,15 @@ def f2u(f):
 # ---------------------------------------------------------------------------------------
 # host-side replicas of the C++ helpers (kernel_fa2_optimized_f16.cu)
 # ---------------------------------------------------------------------------------------
+def swz_bwd(D, r):
+    """f-attn2-backward_f16.cu's Swz<D> (conflict-free for both MFMA shapes)"""
+    if D == 32:
+        return ((r >> 2) & 1) | ((((r >> 2) ^ (r >> 3)) & 1) << 1)
+    if D == 64:
+        return ((r >> 1) & 1) | ((((r >> 1) ^ (r >> 2)) & 1) << 1) | ((((r >> 1) ^ (r >> 3)) & 1) << 2)
+    return (r & 1) | (((r >> 1) & 1) << 1) | (((r ^ (r >> 2)) & 1) << 2) | (((r ^ (r >> 1) ^ (r >> 3)) & 1) << 3)
+
+
 def swz(D, r):
     if D == 32:
         return ((r >> 2) & 1) | (((r >> 3) & 1) << 1)
@@ -68,8 +77,11 @@ def swz(D, r):
     return (r & 1) | (((r >> 1) & 1) << 1) | (((r ^ (r >> 2)) & 1) << 2) | ((((r >> 1) ^ (r >> 3)) & 1) << 3)
 
 
+SWZ = [swz]
+
+
 def tile_off(D, row, col):
-    return row * D + (((col >> 3) ^ swz(D, row)) << 3) + (col & 7)
+    return row * D + (((col >> 3) ^ SWZ[0](D, row)) << 3) + (col & 7)
 
 
 class Sim:
@@ -131,7 +143,7 @@ class Sim:
                 row, ch = x // CPR, x % CPR
                 vo.append((row * D + ch * 8) * 4)
                 if c == 0:
-                    lo = 2 * np.array([row[l] * D + ((ch[l] ^ swz(D, int(row[l]))) << 3) for l in lanes])
+                    lo = 2 * np.array([row[l] * D + ((ch[l] ^ SWZ[0](D, int(row[l]))) << 3) for l in lanes])
             ops = {"qb": 4 * TB * 2 + w * 64 * D * 2, "cnt": self.S // 64 - 1, "goff": 64 * D * 4, "flg": 0,
                    "oa": ((w * 64 + r) * cfg.OST + 4 * h) * 4, "lo": lo, "rsk": "K", "rsv": "V"}
             for t in range(D // 16):
@@ -168,11 +180,72 @@ class Sim:
                     LSE[R] = m[q] * np.log(2.0) + np.log(lt[q])
         return O, LSE, flag, waves
 
-    def asm_text(self):
-        path = os.path.join(HERE, "..", "kernels", "fa2_fwd_hs.inc")
+    def run_dq(self, dO, LSE, Delta):
+        """fa2_bwd_dq_hs_kernel<64>: the C++ prologue, the asm of fa2_bwd_dq_hs.inc, the dQ rows"""
+        import gen_bwd_dq as GD
+        SWZ[0] = swz_bwd
+        D = self.D
+        cfg = GD.Cfg(D, self.bf16)
+        TB = 64 * D
+        self.lds = np.zeros(cfg.lds_bytes // 4, np.uint32)
+        q0 = self.block * 256
+        self.stage(self.Q, q0, 256, 4 * TB, np.float32(LOG2E / np.sqrt(D)))
+        self.stage(dO, q0, 256, 8 * TB, np.float32(1.0))
+        self.stage(self.K, 0, 64, 0, np.float32(1.0))
+        self.stage(self.V, 0, 64, 2 * TB, np.float32(1.0))
+        lanes = np.arange(64)
+        r, h = lanes & 31, lanes >> 5
+        g, i16 = lanes >> 4, lanes & 15
+        ka = [np.array([2 * tile_off(D, int(r[l]), 16 * t + 8 * int(h[l])) for l in lanes]) for t in range(D // 16)]
+        rt = 4 * (g >> 1) + (i16 >> 2)
+        ct = 16 * (g & 1) + 4 * (i16 & 3)
+        kt = [[np.array([2 * tile_off(D, int(rt[l]) + 8 * k, 32 * b + int(ct[l])) for l in lanes]) for k in range(2)]
+              for b in range(D // 32)]
+        text = self.asm_text("fa2_bwd_dq_hs.inc", "FA2_DQ_ASM")
+        waves = []
+        for w in range(4):
+            tid = 64 * w + lanes
+            CPR = D // 8
+            vo, lo = [], None
+            for c in range(D // 32):
+                x = tid + 256 * c
+                row, ch = x // CPR, x % CPR
+                vo.append((row * D + ch * 8) * 4)
+                if c == 0:
+                    lo = 2 * np.array([row[l] * D + ((ch[l] ^ SWZ[0](D, int(row[l]))) << 3) for l in lanes])
+            ops = {"qb": 4 * TB * 2 + w * 64 * D * 2, "db": 8 * TB * 2 + w * 64 * D * 2, "cnt": self.S // 64 - 1,
+                   "goff": 64 * D * 4, "oa": ((w * 64 + r) * cfg.OST + 4 * h) * 4, "lo": lo, "rsk": "K", "rsv": "V"}
+            for c in range(2):
+                qq = q0 + w * 64 + c * 32 + r
+                ok = qq < self.S
+                nl = np.where(ok, -LSE[np.minimum(qq, self.S - 1)] * LOG2E, -np.inf).astype(np.float32)
+                nd = np.where(ok, -Delta[np.minimum(qq, self.S - 1)], 0).astype(np.float32)
+                ops[f"nl{c}"], ops[f"nd{c}"] = f2u(nl), f2u(nd)
+            for t in range(D // 16):
+                ops[f"ka{t}"] = ka[t]
+            for b in range(D // 32):
+                for k in range(2):
+                    ops[f"kt{b}_{k}"] = kt[b][k]
+            for c in range(D // 32):
+                ops[f"vo{c}"] = vo[c]
+            waves.append(Wave(self, w, text, ops))
+        gens = [wv.execute() for wv in waves]
+        while True:
+            states = [next(gn, "done") for gn in gens]
+            if "done" in states:
+                assert all(st == "done" for st in states), f"barrier mismatch: {states}"
+                break
+        dQ = np.zeros((256, D), np.float32)
+        for R_ in range(256):
+            dQ[R_] = u2f(self.lds[R_ * cfg.OST: R_ * cfg.OST + D]) / np.sqrt(D)
+        SWZ[0] = swz
+        return dQ
+
+    def asm_text(self, inc="fa2_fwd_hs.inc", macro="FA2_HS_ASM"):
+        path = os.path.join(HERE, "..", "kernels", inc)
         tag = f"D{self.D}_{'BF16' if self.bf16 else 'F16'}"
         src = open(path).read()
-        blk = src.split(f"#define FA2_HS_ASM_{tag} \\\n")[1].split('    ""')[0]
+        blk = src.split(f"#define {macro}_{tag} \\\n")[1].split('    ""')[0]
         lines = [ln.strip()[1:].split("\\n")[0] for ln in blk.splitlines() if ln.strip().startswith('"')]
         return [ln.replace("%=", "0") for ln in lines]
 
@@ -310,13 +383,15 @@ class Wave:
                 x = u2f(self.vsrc(args[1]))
                 with np.errstate(over="ignore"):
                     self.put(f, k, f2u(np.exp2(x.astype(np.float64)).astype(np.float32)))
-            elif op in ("v_add_f32", "v_sub_f32", "v_max_f32", "v_max3_f32"):
+            elif op in ("v_add_f32", "v_sub_f32", "v_max_f32", "v_max3_f32", "v_mul_f32"):
                 (f, k), = self.regs(args[0])
                 xs = [u2f(self.vsrc(a)).astype(np.float32) for a in args[1:]]
                 if op == "v_add_f32":
                     y = xs[0] + xs[1]
                 elif op == "v_sub_f32":
                     y = xs[0] - xs[1]
+                elif op == "v_mul_f32":
+                    y = xs[0] * xs[1]
                 else:
                     y = np.maximum.reduce(xs)
                 self.put(f, k, f2u(y))
@@ -401,10 +476,30 @@ def main():
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--spike", action="store_true")
     ap.add_argument("--block", type=int, default=0)
+    ap.add_argument("--kernel", choices=["fwd", "dq"], default="fwd")
     a = ap.parse_args()
     rng = np.random.RandomState(0)
     S, D = a.S, a.D
     Q, K, V = (rng.rand(S, D).astype(np.float32) for _ in range(3))
+    if a.kernel == "dq":
+        dO = rng.randn(S, D).astype(np.float32)
+        s64 = (Q.astype(np.float64) @ K.T.astype(np.float64)) / np.sqrt(D)
+        mx = s64.max(1, keepdims=True)
+        lse = mx[:, 0] + np.log(np.exp(s64 - mx).sum(1))
+        P = np.exp(s64 - lse[:, None])
+        O = P @ V.astype(np.float64)
+        delta = (dO.astype(np.float64) * O).sum(1)
+        dS = P * (dO.astype(np.float64) @ V.T.astype(np.float64) - delta[:, None])
+        edq = dS @ K.astype(np.float64) / np.sqrt(D)
+        sim = Sim(D, a.bf16, S, Q, K, V, a.block)
+        dq = sim.run_dq(dO, lse.astype(np.float32), delta.astype(np.float32))
+        q0 = a.block * 256
+        nq = min(256, S - q0)
+        err = np.abs(dq[:nq] - edq[q0:q0 + nq]).max()
+        scale = max(1.0, np.abs(edq).max())
+        print(f"dQ D={D} S={S} {'bf16' if a.bf16 else 'fp16'} block {a.block}: max|ddQ| {err:.3e} (scale {scale:.2f})")
+        assert err < (2e-2 if a.bf16 else 1e-2) * scale, "mismatch"
+        return
     if a.spike:
         K[S - 3] = 3.0
     sim = Sim(D, a.bf16, S, Q, K, V, a.block)

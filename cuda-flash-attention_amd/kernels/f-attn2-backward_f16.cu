@@ -1511,6 +1511,115 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     }
 }
 
+#ifndef CUPY_INLINE_COMPILE
+// ---------------------------------------------------------------------------
+// Hand-scheduled dQ (D = 64; S % 64 == 0, S >= 128), r05.
+// ---------------------------------------------------------------------------
+// One workgroup = 4 waves = 256 query rows, one wave per SIMD; each wave keeps 64 query
+// rows as two 32-row chains (Q, dO fragments and dQᵀ accumulators in AGPRs) and streams
+// the head's 64-key K/V tiles through LDS.  Per tile four MFMA phases alternate the
+// chains: Sᵀ and dPᵀ of one chain while the other chain's dS is formed in the MFMA gaps,
+// then that chain's dQᵀ += Kᵀ dSᵀ.  The tile loop is the generated inline-asm block of
+// fa2_bwd_dq_hs.inc (gen/gen_bwd_dq.py); this kernel stages the Q and dO blocks, computes
+// Δ = rowsum(dO ∘ O) from the staged rows (O given: written out for the dK/dV kernel) or
+// reads it, hands the asm the lane-constant seeds -LSE·log2e and -Δ, and stores the dQ
+// rows it leaves (unscaled fp32) in an LDS stage.  Every dQ element is summed in one fixed
+// order: bitwise reproducible, no atomics (the reference: f-attn2-backward_f16.cu:240-301).
+}  // namespace fa2f16b
+#include "fa2_bwd_dq_hs.inc"
+namespace fa2f16b {
+
+template <int D>
+__global__ void __launch_bounds__(256, 1)
+fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                     const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
+                     float* __restrict__ dQ, int S, const float* __restrict__ O) {
+    static_assert(D == 64, "hand-scheduled dQ: D = 64");
+    constexpr int KT = 64, TB = KT * D, OST = D + 4;
+    __shared__ __attribute__((aligned(16))) _Float16 smem[FA2_DQ_LDS_D64 / 2];
+    __shared__ float rowc[2][256];  // -LSE*log2e and Δ of the block's rows
+
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nqb = (S + 255) / 256;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = bid / nqb, qb = bid - bh * nqb;
+    const long base = (long)bh * S * D;
+    const long rbase = (long)bh * S;
+    const int qrow0 = qb * 256;
+
+    // Q block (scaled by log2(e)/sqrt(D)) -> LDS [4TB, 8TB) halves; dO block -> [8TB, 12TB)
+    {
+        TileStager<D, 256, 256> qst;
+        qst.init(Q + base, S, tid);
+        qst.load(qrow0);
+        qst.store(smem + 4 * TB, FA2B_LOG2E / __builtin_sqrtf((float)D), tid);
+    }
+    {
+        TileStager<D, 256, 256> dst;
+        dst.init(dO + base, S, tid);
+        dst.load(qrow0);
+        if (O) {
+            TileStager<D, 256, 256> ost;
+            ost.init(O + base, S, tid);
+            ost.load(qrow0);
+            delta_rows<D, 256, 256>(dst, ost, S, qrow0, rowc[1], Delta + rbase, tid);
+        }
+        dst.store(smem + 8 * TB, 1.f, tid);
+    }
+    {
+        const int q = qrow0 + tid;
+        rowc[0][tid] = q < S ? -LSE[rbase + q] * FA2B_LOG2E : -__builtin_inff();
+        if (!O) rowc[1][tid] = q < S ? Delta[rbase + q] : 0.f;
+    }
+    TileStager<D, KT, 256> ks, vs;
+    ks.init(K + base, S, tid);
+    vs.init(V + base, S, tid);
+    ks.load(0);
+    vs.load(0);
+    ks.store(smem, 1.f, tid);
+    vs.store(smem + 2 * TB, 1.f, tid);
+    __syncthreads();
+
+    FragOffsets<D> fo;
+    fo.init(lane);
+    int hs_ka[D / 16], hs_kt[D / 32][2], hs_vo[D / 32];
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) hs_ka[t] = fo.row[t] * 2;
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b) {
+        hs_kt[b][0] = fo.tr[b][0] * 2;
+        hs_kt[b][1] = fo.tr[b][1] * 2;
+    }
+#pragma unroll
+    for (int c = 0; c < D / 32; ++c) hs_vo[c] = ks.voff[c];
+    const int hs_lo = ks.loff[0] * 2;
+    const int hs_oa = ((wave * 64 + r) * OST + 4 * h) * 4;
+    const float hs_nl0 = rowc[0][wave * 64 + r], hs_nl1 = rowc[0][wave * 64 + 32 + r];
+    const float hs_nd0 = -rowc[1][wave * 64 + r], hs_nd1 = -rowc[1][wave * 64 + 32 + r];
+    const __amdgpu_buffer_rsrc_t hs_rsk = ks.rs, hs_rsv = vs.rs;
+    const int hs_qb = __builtin_amdgcn_readfirstlane(4 * TB * 2 + wave * 64 * D * 2);
+    const int hs_db = __builtin_amdgcn_readfirstlane(8 * TB * 2 + wave * 64 * D * 2);
+    int hs_cnt = __builtin_amdgcn_readfirstlane(S / KT - 1);
+    int hs_goff = __builtin_amdgcn_readfirstlane(KT * D * 4);
+#ifdef FA2_TILE_BF16
+    asm volatile(FA2_DQ_ASM_D64_BF16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
+#else
+    asm volatile(FA2_DQ_ASM_D64_F16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
+#endif
+    // dQ rows [wave*64 + c*32 + q][OST] (unscaled) -> HBM as whole rows, times 1/sqrt(D)
+    constexpr int LPR = D / 4, RPI = 64 / LPR;
+    const float dscale = 1.f / __builtin_sqrtf((float)D);
+    const float* os = reinterpret_cast<const float*>(smem);
+#pragma unroll 4
+    for (int rr = 0; rr < 64; rr += RPI) {
+        const int row = wave * 64 + rr + lane / LPR, c4 = (lane % LPR) * 4;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(os + row * OST + c4) * dscale;
+        if (qrow0 + row < S) *reinterpret_cast<f32x4*>(dQ + base + (long)(qrow0 + row) * D + c4) = v;
+    }
+}
+#endif  // CUPY_INLINE_COMPILE
+
 template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1, bool PIPE = false>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
@@ -1860,6 +1969,21 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     // tiles with the 4-tile staging registers spill).  Measured (B2_H8_D64 dQ + Δ,
     // r01): S = 512 17.0 -> 11.4 us, 1024 29.5 -> 15.7, 2048 41.9 -> 36.7.
     int ksp = tune_knob("DQ_KS", 0);
+    if constexpr (D == 64) {
+        // hand-scheduled kernel (r05): whole 64-key tiles, and a grid of at least one
+        // 256-row workgroup per CU.  DQ_HS (tests and tools): 1 forces it (an error where it
+        // cannot serve), 0 disables it
+        const int hs = tune_knob("DQ_HS", -1);
+        const bool fits = S % 64 == 0 && S >= 128;
+        if (hs == 1 && !fits) return hipErrorInvalidValue;
+        const long hgrid = (long)bh * ((S + 255) / 256);
+        if (fits && (hs == 1 || (hs < 0 && nw == 0 && ksp == 0 && !tune_knob("DQ_PIPE", 0) && hgrid >= cu_count()))) {
+            if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D>), dim3((unsigned)hgrid), dim3(256), 0, stream, q, k, v,
+                               dout, lse, delta, dq, S, o);
+            return hipGetLastError();
+        }
+    }
     if (ksp == 0 && nw == 0 && D <= 64) {
         const int a = auto_waves(units, 8);
         if (a == 4) ksp = 2, nw = 8;

@@ -1,0 +1,118 @@
+"""GPU parity of the hand-scheduled backward kernels (r05) against the oracle.
+
+fa2_bwd_dq_hs_kernel<64> (generated asm loop, gen/gen_bwd_dq.py) computes dQ (and Δ, when
+it gets O) for D = 64 on whole 64-key tiles; it is the default dQ launch wherever its grid
+holds at least one 256-row workgroup per CU (C3, C5, the S = 4096 sweep point).  DQ_HS = 1
+forces it onto the small shapes here: one and several 256-row blocks per head, a last
+block with rows past S, N(0,1) inputs and gradients, both tile types, Δ fused (O given)
+and Δ supplied.  Tolerances are the north star's (1e-2 fp16, 2e-2 bf16, gradients scaled
+by max(1, max|ref|) as in test_gpu_parity.py).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import fa2amd  # noqa: E402
+from oracle import fa2_oracle as fo  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+TOL = {"fp16": 1e-2, "bf16": 2e-2}
+
+
+def cuda(*xs):
+    return [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in xs]
+
+
+def maxerr(a, b):
+    return float(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)).max())
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    fa2amd.lib()
+
+
+@pytest.fixture(autouse=True)
+def _no_overrides():
+    fa2amd.tune_set(None)
+    yield
+    fa2amd.tune_set(None)
+
+
+DQ_SHAPES = [(1, 1, 128, 64), (1, 2, 192, 64), (2, 1, 256, 64), (1, 2, 320, 64), (1, 3, 832, 64), (1, 1, 2048, 64)]
+
+
+def _case(shape, seed=3, gauss=False):
+    B, H, S, D = shape
+    q, k, v = (fo.cli_inputs if gauss else fo.harness_inputs)(B, H, S, D, seed=seed)
+    do = np.random.RandomState(seed + 1).randn(B, H, S, D).astype(np.float32)
+    eo, el = fo.attention_forward(q, k, v)
+    edq, edk, edv, edl = fo.attention_backward(q, k, v, do)
+    return (q, k, v, do, eo.astype(np.float32), el.astype(np.float32)), (edq, edk, edv, edl)
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+@pytest.mark.parametrize("shape", DQ_SHAPES, ids=lambda s: "B%d_H%d_S%d_D%d" % s)
+def test_hs_dq_full_backward(shape, precision):
+    """fa2_backward's two-kernel plan with the hand-scheduled dQ (Δ fused, written out for dK/dV)"""
+    fa2amd.tune_set("DQ_HS", 1)
+    fa2amd.tune_set("BWD_FUSED", 0)
+    (q, k, v, do, o, lse), (edq, edk, edv, _) = _case(shape)
+    tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
+    dq, dk, dv = fa2amd.backward(tq, tk, tv, to, tdo, tl, precision)
+    torch.cuda.synchronize()
+    for got, exp in ((dq, edq), (dk, edk), (dv, edv)):
+        g = got.cpu().numpy()
+        assert np.isfinite(g).all()
+        assert maxerr(g, exp) < TOL[precision] * max(1.0, float(np.abs(exp).max()))
+
+
+@pytest.mark.parametrize("fused_delta", [True, False], ids=["delta_fused", "delta_given"])
+@pytest.mark.parametrize("shape", [(1, 2, 320, 64), (2, 2, 1024, 64)], ids=lambda s: "B%d_H%d_S%d_D%d" % s)
+def test_hs_dq_entry_points(shape, fused_delta):
+    """fa2_backward_dq_delta (Δ from the staged O rows, written out) and fa2_backward_dq (Δ read)"""
+    fa2amd.tune_set("DQ_HS", 1)
+    (q, k, v, do, o, lse), (edq, _, _, edl) = _case(shape, seed=7, gauss=True)
+    tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
+    dq = torch.empty_like(tq)
+    if fused_delta:
+        dl = torch.full(tl.shape, float("nan"), device=tq.device)
+        fa2amd.backward_dq_delta(tq, tk, tv, to, tdo, tl, dl, dq)
+    else:
+        dl = fa2amd.delta(tdo, to)
+        fa2amd.backward_dq(tq, tk, tv, tdo, tl, dl, dq)
+    torch.cuda.synchronize()
+    assert maxerr(dl.cpu().numpy(), edl) < 1e-4 * max(1.0, float(np.abs(edl).max()))
+    assert maxerr(dq.cpu().numpy(), edq) < TOL["fp16"] * max(1.0, float(np.abs(edq).max()))
+
+
+def test_hs_dq_deterministic_and_default():
+    """bitwise repeatable; at C3's grid the default dQ launch is the hand-scheduled one"""
+    B, H, S, D = 4, 16, 2048, 64
+    q, k, v = fo.harness_inputs(B, H, S, D, seed=2)
+    do = np.random.RandomState(9).randn(B, H, S, D).astype(np.float32)
+    tq, tk, tv, tdo = cuda(q, k, v, do)
+    o, lse = fa2amd.forward(tq, tk, tv, "fp16")
+    res = []
+    for hs in (-1, 1, 1, 0):
+        fa2amd.tune_set("DQ_HS", hs)
+        dq, dk, dv = fa2amd.backward(tq, tk, tv, o, tdo, lse, "fp16")
+        torch.cuda.synchronize()
+        res.append(dq.cpu().numpy())
+    assert np.array_equal(res[0], res[1]) and np.array_equal(res[1], res[2])
+    assert maxerr(res[1], res[3]) < 2e-3 * max(1.0, float(np.abs(res[3]).max()))
+    edq, _, _, _ = fo.attention_backward(q[:1, :2], k[:1, :2], v[:1, :2], do[:1, :2])
+    assert maxerr(res[1][:1, :2], edq) < TOL["fp16"] * max(1.0, float(np.abs(edq).max()))
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 100, 64), (1, 1, 64, 64)])
+def test_hs_dq_forced_on_unserved_shape_is_an_error(shape):
+    fa2amd.tune_set("DQ_HS", 1)
+    fa2amd.tune_set("BWD_FUSED", 0)
+    (q, k, v, do, o, lse), _ = _case(shape)
+    tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
+    with pytest.raises(fa2amd.FA2Error):
+        fa2amd.backward(tq, tk, tv, to, tdo, tl, "fp16")
