@@ -113,44 +113,61 @@ def regs_of(ins):
 
 def insert_waits(seq, state):
     """state: (lgkm list, vm list) of outstanding ops as frozensets of written regs"""
-    lg, vm = [list(state[0]), list(state[1])]
+    out, ends = insert_waits_multi(seq, [state])
+    return out, ends[0]
+
+
+def insert_waits_multi(seq, states):
+    """counted waits valid for every entry state in `states` (each (lgkm, vm) as above): before
+    each consumer the smallest count any state needs; returns (seq, exit states)"""
+    sts = [[list(st[0]), list(st[1])] for st in states]
     out = []
+
+    def retire(q, n):
+        return q[len(q) - n:] if n < len(q) else q
+
     for ins in seq:
         if ins.kind == "wait":
             t = ins.text
-            if "lgkmcnt(" in t:
-                n = int(t.split("lgkmcnt(")[1].split(")")[0])
-                lg = lg[len(lg) - n:] if n < len(lg) else lg
-            if "vmcnt(" in t:
-                n = int(t.split("vmcnt(")[1].split(")")[0])
-                vm = vm[len(vm) - n:] if n < len(vm) else vm
+            for st in sts:
+                if "lgkmcnt(" in t:
+                    st[0] = retire(st[0], int(t.split("lgkmcnt(")[1].split(")")[0]))
+                if "vmcnt(" in t:
+                    st[1] = retire(st[1], int(t.split("vmcnt(")[1].split(")")[0]))
             out.append(ins)
             continue
         touched = regs_of(ins)
         nl = nv = None
-        for idx, e in enumerate(lg):
-            if e & touched:
-                nl = len(lg) - idx - 1
-        for idx, e in enumerate(vm):
-            if e & touched:
-                nv = len(vm) - idx - 1
+        for st in sts:
+            for idx, e in enumerate(st[0]):
+                if e & touched:
+                    n = len(st[0]) - idx - 1
+                    nl = n if nl is None else min(nl, n)
+            for idx, e in enumerate(st[1]):
+                if e & touched:
+                    n = len(st[1]) - idx - 1
+                    nv = n if nv is None else min(nv, n)
         parts = []
         if nv is not None:
             nv = min(nv, 63)
             parts.append(f"vmcnt({nv})")
-            vm = vm[len(vm) - nv:] if nv else []
         if nl is not None:
             nl = min(nl, 15)
             parts.append(f"lgkmcnt({nl})")
-            lg = lg[len(lg) - nl:] if nl else []
+        for st in sts:
+            if nv is not None:
+                st[1] = retire(st[1], nv) if nv else []
+            if nl is not None:
+                st[0] = retire(st[0], nl) if nl else []
         if parts:
             out.append(Ins("s_waitcnt " + " ".join(parts), "wait"))
         out.append(ins)
-        if ins.kind in ("dsr", "dsw"):
-            lg.append(frozenset(ins.wr))
-        elif ins.kind == "vmem":
-            vm.append(frozenset(ins.wr))
-    return out, (tuple(lg), tuple(vm))
+        for st in sts:
+            if ins.kind in ("dsr", "dsw"):
+                st[0].append(frozenset(ins.wr))
+            elif ins.kind == "vmem":
+                st[1].append(frozenset(ins.wr))
+    return out, [(tuple(st[0]), tuple(st[1])) for st in sts]
 
 
 def mfma_result_ws(ins):

@@ -92,6 +92,7 @@ class Sim:
         self.lds = np.zeros(cfg.lds_bytes // 4, np.uint32)  # dword-addressed
         self.Q, self.K, self.V = Q, K, V  # one head [S][D] float32
         self.block = block
+        self.tensors = {"K": K, "V": V, "Q": Q}
         self.to16 = f2bf if bf16 else f2h
         self.from16 = bf2f if bf16 else h2f
 
@@ -241,6 +242,72 @@ class Sim:
         SWZ[0] = swz
         return dQ
 
+    def run_dkdv(self, dO, LSE, Delta):
+        """fa2_bwd_dkdv_hs_kernel<64>: the C++ prologue, the asm of fa2_bwd_dkdv_hs.inc, dK and dV rows"""
+        import gen_bwd_dkdv as GK
+        SWZ[0] = swz_bwd
+        D = self.D
+        cfg = GK.Cfg(D, self.bf16)
+        TB = 64 * D
+        self.lds = np.zeros(cfg.lds_bytes // 4, np.uint32)
+        self.tensors.update({"dO": dO, "LSE": LSE, "Delta": Delta, "null": np.zeros(0, np.float32)})
+        k0 = self.block * 256
+        self.stage(self.K, k0, 256, cfg.KVB // 2, np.float32(LOG2E / np.sqrt(D)))
+        self.stage(self.V, k0, 256, cfg.KVB // 2 + 256 * D, np.float32(1.0))
+        self.stage(self.Q, 0, 64, 0, np.float32(1.0))
+        self.stage(dO, 0, 64, TB, np.float32(1.0))
+        for q in range(64):
+            ok = q < self.S
+            self.lds[(cfg.RC >> 2) + q] = f2u(np.float32(-LSE[q] * LOG2E if ok else 0.0))
+            self.lds[(cfg.RC >> 2) + 64 + q] = f2u(np.float32(-Delta[q] if ok else 0.0))
+        lanes = np.arange(64)
+        r, h = lanes & 31, lanes >> 5
+        g, i16 = lanes >> 4, lanes & 15
+        ka = [np.array([2 * tile_off(D, int(r[l]), 16 * t + 8 * int(h[l])) for l in lanes]) for t in range(D // 16)]
+        rt = 4 * (g >> 1) + (i16 >> 2)
+        ct = 16 * (g & 1) + 4 * (i16 & 3)
+        tr = [[np.array([2 * tile_off(D, int(rt[l]) + 8 * k, 32 * b + int(ct[l])) for l in lanes]) for k in range(2)]
+              for b in range(D // 32)]
+        text = self.asm_text("fa2_bwd_dkdv_hs.inc", "FA2_DK_ASM")
+        waves = []
+        for w in range(4):
+            tid = 64 * w + lanes
+            CPR = D // 8
+            vo, lo = [], None
+            for c in range(D // 32):
+                x = tid + 256 * c
+                row, ch = x // CPR, x % CPR
+                vo.append((row * D + ch * 8) * 4)
+                if c == 0:
+                    lo = 2 * np.array([row[l] * D + ((ch[l] ^ SWZ[0](D, int(row[l]))) << 3) for l in lanes])
+            oak = ((w * 64 + r) * cfg.OST + 4 * h) * 4
+            ops = {"cnt": self.S // 64 - 1, "goff": 64 * D * 4, "roff": 256, "lo": lo, "rco": 16 * h,
+                   "rvo": 4 * lanes, "rcw": (256 * w if w < 2 else 512) + 4 * lanes, "oak": oak,
+                   "oav": oak + 256 * cfg.OST * 4, "rsq": "Q", "rsd": "dO",
+                   "rsc": ["LSE", "Delta", "null", "null"][w],
+                   "rsm": int(f2u(np.float32([-LOG2E, -1.0, 0.0, 0.0][w]))), "kvb": cfg.KVB + w * 64 * D * 2}
+            for t in range(D // 16):
+                ops[f"ka{t}"] = ka[t]
+            for b in range(D // 32):
+                for k in range(2):
+                    ops[f"tr{b}_{k}"] = tr[b][k]
+            for c in range(D // 32):
+                ops[f"vo{c}"] = vo[c]
+            waves.append(Wave(self, w, text, ops))
+        gens = [wv.execute() for wv in waves]
+        while True:
+            states = [next(gn, "done") for gn in gens]
+            if "done" in states:
+                assert all(st == "done" for st in states), f"barrier mismatch: {states}"
+                break
+        dK = np.zeros((256, D), np.float32)
+        dV = np.zeros((256, D), np.float32)
+        for R_ in range(256):
+            dK[R_] = u2f(self.lds[R_ * cfg.OST: R_ * cfg.OST + D]) / np.sqrt(D)
+            dV[R_] = u2f(self.lds[(256 + R_) * cfg.OST: (256 + R_) * cfg.OST + D])
+        SWZ[0] = swz
+        return dK, dV
+
     def asm_text(self, inc="fa2_fwd_hs.inc", macro="FA2_HS_ASM"):
         path = os.path.join(HERE, "..", "kernels", inc)
         tag = f"D{self.D}_{'BF16' if self.bf16 else 'F16'}"
@@ -339,7 +406,7 @@ class Wave:
             elif op == "buffer_load_dwordx4":
                 dst = self.regs(args[0])
                 voff = self.vsrc(args[1]).astype(np.int64)
-                tens = {"K": sim.K, "V": sim.V}[self.ops[args[2][2:-1]]]
+                tens = sim.tensors[self.ops[args[2][2:-1]]]
                 soff = int(self.ops[args[3].split()[0][2:-1]])
                 imm = int(args[3].split("offset:")[1]) if "offset:" in args[3] else 0
                 flat = tens.reshape(-1)
@@ -350,6 +417,24 @@ class Wave:
                     ok = (addr + 4 * e + 4) <= flat.size * 4
                     data[e] = np.where(ok, f2u(flat[np.minimum(idx, flat.size - 1)]), 0)
                 self.issue(self.vm, dst, data)
+            elif op == "buffer_load_dword":
+                dst = self.regs(args[0])
+                voff = self.vsrc(args[1]).astype(np.int64)
+                flat = sim.tensors[self.ops[args[2][2:-1]]].reshape(-1)
+                soff = int(self.ops[args[3].split()[0][2:-1]])
+                addr = voff + soff
+                ok = (addr + 4) <= flat.size * 4
+                data = np.where(ok, f2u(flat[np.minimum(addr // 4, max(flat.size - 1, 0))]) if flat.size else 0, 0)
+                self.issue(self.vm, dst, np.asarray(data, np.uint32).reshape(1, 64))
+            elif op == "ds_write_b32":
+                dtok, _, offs = args[1].partition(" offset:")
+                addr = self.vsrc(args[0]).astype(np.int64) + (int(offs) if offs else 0)
+                src = self.vsrc(dtok)
+                for l in range(64):
+                    sim.lds[int(addr[l]) >> 2] = src[l]
+                self.lgkm.append(([], lambda: None))
+            elif op == "s_branch":
+                self.pc = self.labels[args[0]]
             elif op in ("ds_read_b128", "ds_read_b64_tr_b16"):
                 dst = self.regs(args[0])
                 tok, _, offs = args[1].partition(" offset:")
@@ -476,11 +561,32 @@ def main():
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--spike", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", choices=["fwd", "dq"], default="fwd")
+    ap.add_argument("--kernel", choices=["fwd", "dq", "dkdv"], default="fwd")
     a = ap.parse_args()
     rng = np.random.RandomState(0)
     S, D = a.S, a.D
     Q, K, V = (rng.rand(S, D).astype(np.float32) for _ in range(3))
+    if a.kernel == "dkdv":
+        dO = rng.randn(S, D).astype(np.float32)
+        s64 = (Q.astype(np.float64) @ K.T.astype(np.float64)) / np.sqrt(D)
+        mx = s64.max(1, keepdims=True)
+        lse = mx[:, 0] + np.log(np.exp(s64 - mx).sum(1))
+        P = np.exp(s64 - lse[:, None])
+        O = P @ V.astype(np.float64)
+        delta = (dO.astype(np.float64) * O).sum(1)
+        dS = P * (dO.astype(np.float64) @ V.T.astype(np.float64) - delta[:, None])
+        edk = dS.T @ Q.astype(np.float64) / np.sqrt(D)
+        edv = P.T @ dO.astype(np.float64)
+        sim = Sim(D, a.bf16, S, Q, K, V, a.block)
+        dk, dv = sim.run_dkdv(dO, lse.astype(np.float32), delta.astype(np.float32))
+        k0 = a.block * 256
+        nk = min(256, S - k0)
+        ek = np.abs(dk[:nk] - edk[k0:k0 + nk]).max() / max(1.0, np.abs(edk).max())
+        ev = np.abs(dv[:nk] - edv[k0:k0 + nk]).max() / max(1.0, np.abs(edv).max())
+        print(f"dKdV D={D} S={S} {'bf16' if a.bf16 else 'fp16'} block {a.block}: rel max|ddK| {ek:.3e}, |ddV| {ev:.3e}")
+        tol = 2e-2 if a.bf16 else 1e-2
+        assert ek < tol and ev < tol, "mismatch"
+        return
     if a.kernel == "dq":
         dO = rng.randn(S, D).astype(np.float32)
         s64 = (Q.astype(np.float64) @ K.T.astype(np.float64)) / np.sqrt(D)

@@ -1,0 +1,449 @@
+#!/usr/bin/env python3
+"""Generator of the hand-scheduled FA2 backward dK/dV loop for gfx950 (MI355X), D = 64.
+
+Writes ../kernels/fa2_bwd_dkdv_hs.inc: the inline-asm body of `fa2_bwd_dkdv_hs_kernel<64>`
+(f-attn2-backward_f16.cu), between its C++ prologue (the workgroup's K block, scaled by
+log2(e)/sqrt(D), and V block; the first 64-query step's Q, dO and row constants) and its
+C++ epilogue (dK, dV rows from an LDS stage; dK times 1/sqrt(D)).  The math is the dK/dV
+part of the reference's backward (kernels/f-attn2-backward_f16.cu:170-268):
+P = exp(Q K^T / sqrt(D) - LSE), dV = P^T dO, dS = P o (dO V^T - Delta), dK = dS^T Q / sqrt(D):
+
+  * one workgroup = 4 waves = 256 keys, ONE wave per SIMD; each wave holds 64 keys as two
+    32-key chains A and B: their K and V fragments and dK^T / dV^T accumulators sit in
+    AGPRs for the whole query loop;
+  * the head's queries stream in 64-row steps (Q and dO as fp16/bf16 tiles, -LSE*log2e and
+    -Delta rows) through a 3-slot LDS ring, one barrier per step; per step four phases:
+        P1  S, dP of A (step j)        | P, dS of B (step j-1), query block 1
+        P2  dV^T, dK^T of B (step j-1)| P, dS of A (step j),   query block 0
+        P3  S, dP of B (step j)        | P, dS of A (step j),   query block 1   -> barrier
+        P4  dV^T, dK^T of A (step j)  | P, dS of B (step j),   query block 0
+  * S = Q K^T starts from -LSE*log2e and dP = dO V^T from -Delta (16-register row-constant
+    tuples read from LDS into a 2-slot ring: the query is on the accumulator rows), so
+    P = exp2(acc) and dS = P * acc; P and dS are packed in place and ARE the B operands
+    of dV^T += dO^T P and dK^T += Q^T dS (dO^T, Q^T through ds_read_b64_tr_b16 into an
+    8-slot ring);
+  * Q and dO rows: fp32 HBM -> registers -> fp16/bf16 -> swizzled LDS two steps ahead of
+    their use; the row constants by one dword load per lane of waves 0 (LSE) and 1 (Delta).
+
+Register map (D = 64):
+  AGPR  dK^T[c][b] a[16(2c+b)]    dV^T[c][b] a[64+16(2c+b)]
+        K[c][t]    a[128+4(4c+t)] V[c][t]    a[160+4(4c+t)]
+        Q rows     a[192+4(4qb+t)] dO rows   a[224+4(4qb+t)]
+  VGPR  S[c][qb]   v[32c+16qb]    dP[c][qb]  v[64+32c+16qb]
+        seed ring  v[128..159]    trop ring  v[160..191]   staging v[192..223]  row const v[224]
+
+Usage: python3 gen_bwd_dkdv.py [--check]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from asmgen import Ins, R, fix_hazards, insert_waits, insert_waits_multi, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402,E501
+
+QT = 64  # queries per step
+KEYS = 256  # keys per workgroup
+
+
+class Cfg:
+    def __init__(self, D, bf16):
+        assert D == 64
+        self.D, self.bf16 = D, bf16
+        self.NB, self.NTQ, self.CPT = D // 32, D // 16, D // 32
+        self.exp_per_gap = 1
+        self.TBB = QT * D * 2  # one 16-bit [64][D] tile
+        # a slot: Q, dO tiles + row constants -LSE*log2e, -Delta (and a 256-B sink that waves
+        # 2 and 3 write: every wave runs the same staging code)
+        self.SLOT = 2 * self.TBB + 768
+        self.RC = 2 * self.TBB  # row constants inside a slot
+        self.KVB = 3 * self.SLOT  # K block, then V block (256 rows each)
+        self.OST = D + 4
+        self.mf = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
+        self.cvt = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
+        self.nvgpr, self.nagpr = 226, 256
+
+    # AGPRs
+    def dK(self, c, b):
+        return 16 * (2 * c + b)
+
+    def dV(self, c, b):
+        return 64 + 16 * (2 * c + b)
+
+    def Kf(self, c, t):
+        return 128 + 4 * (4 * c + t)
+
+    def Vf(self, c, t):
+        return 160 + 4 * (4 * c + t)
+
+    def Qr(self, qb, t):
+        return 192 + 4 * (4 * qb + t)
+
+    def dOr(self, qb, t):
+        return 224 + 4 * (4 * qb + t)
+
+    # VGPRs
+    def S(self, c, qb, i=0):
+        return 32 * c + 16 * qb + i
+
+    def dP(self, c, qb, i=0):
+        return 64 + 32 * c + 16 * qb + i
+
+    def seed(self, k):
+        return 128 + 16 * k
+
+    def tr(self, k):
+        return 160 + 4 * k
+
+    def stg(self, tensor, cc):
+        return 192 + 8 * (tensor * self.CPT + cc)
+
+    RCV = 224
+
+    @property
+    def lds_bytes(self):
+        stage = 2 * KEYS * self.OST * 4
+        return max(self.KVB + 2 * KEYS * self.D * 2, stage)
+
+
+def mfma(cfg, dst, a, b, c, c_is_zero=False):
+    rd = R(rng(a[0], a[1], 4), "A") + R(rng(b[0], b[1], 4), "B")
+    if not c_is_zero:
+        rd += R(rng(c[0], c[1], 16), "C")
+    ctxt = "0" if c_is_zero else rtxt(c[0], c[1], 16)
+    return Ins(f"{cfg.mf} {rtxt(dst[0], dst[1], 16)}, {rtxt(a[0], a[1], 4)}, {rtxt(b[0], b[1], 4)}, {ctxt}", "mfma",
+               rd, rng(dst[0], dst[1], 16))
+
+
+# ---- LDS reads --------------------------------------------------------------------------
+def rowop_reads(cfg, slot):
+    """Q and dO row fragments (qb, t) of the step in `slot` -> AGPRs (A operands of S, dP)"""
+    out = []
+    for tensor in range(2):
+        for qb in range(2):
+            for t in range(cfg.NTQ):
+                d = cfg.Qr(qb, t) if tensor == 0 else cfg.dOr(qb, t)
+                off = slot * cfg.SLOT + tensor * cfg.TBB + qb * 32 * cfg.D * 2
+                out.append(Ins(f"ds_read_b128 {rtxt('a', d, 4)}, %[ka{t}] offset:{off}", "dsr", [], rng("a", d, 4)))
+    return tagged("lds", out)
+
+
+def seed_reads(cfg, slot, which, qb, k, earliest=0, deadline=None):
+    """row-constant tuple (which 0: -LSE*log2e, 1: -Delta) of query block qb -> seed ring slot k:
+    register 4g+e holds the row qb*32 + 8g + 4h + e"""
+    out = []
+    base = slot * cfg.SLOT + cfg.RC + which * 256 + qb * 128
+    d = cfg.seed(k)
+    for g in range(4):
+        out.append(Ins(f"ds_read_b128 {rtxt('v', d + 4 * g, 4)}, %[rco] offset:{base + 32 * g}", "dsr", [],
+                       rng("v", d + 4 * g, 4), earliest=earliest, deadline=deadline))
+    return tagged("lds", out)
+
+
+def trop_frag(cfg, k):
+    """the k-th A operand of a dV^T / dK^T phase: (tensor, b, qb, s)"""
+    b, rest = k // 8, k % 8
+    tensor = rest // 4  # 0: dO^T (for dV), 1: Q^T (for dK)
+    qb, s = (rest % 4) // 2, rest % 2
+    return tensor, b, qb, s
+
+
+def trop_reads(cfg, slot, k, earliest=0, deadline=None):
+    tensor, b, qb, s = trop_frag(cfg, k)
+    tt = 1 if tensor == 0 else 0  # LDS tile: 0 = Q, 1 = dO
+    off = slot * cfg.SLOT + tt * cfg.TBB + (qb * 32 + 16 * s) * cfg.D * 2
+    d = cfg.tr(k % 8)
+    return tagged("lds", [
+        Ins(f"ds_read_b64_tr_b16 {rtxt('v', d, 2)}, %[tr{b}_0] offset:{off}", "dsr", [], rng("v", d, 2),
+            earliest=earliest, deadline=deadline),
+        Ins(f"ds_read_b64_tr_b16 {rtxt('v', d + 2, 2)}, %[tr{b}_1] offset:{off}", "dsr", [], rng("v", d + 2, 2),
+            earliest=earliest, deadline=deadline)])
+
+
+# ---- MFMA chains -------------------------------------------------------------------------
+SEED_ORDER = [(0, 0, 0), (1, 0, 1), (0, 1, 0), (1, 1, 1)]  # (which, qb, ring slot) in MFMA order
+
+
+def sdp_mfmas(cfg, c):
+    """S[c][qb] = Q K^T - LSE*log2e, dP[c][qb] = dO V^T - Delta: S qb0, dP qb0, S qb1, dP qb1"""
+    out = []
+    for which, qb, k in SEED_ORDER:
+        for t in range(cfg.NTQ):
+            if which == 0:
+                dst, a, b = cfg.S(c, qb), cfg.Qr(qb, t), cfg.Kf(c, t)
+            else:
+                dst, a, b = cfg.dP(c, qb), cfg.dOr(qb, t), cfg.Vf(c, t)
+            cc = ("v", cfg.seed(k)) if t == 0 else ("v", dst)
+            out.append(mfma(cfg, ("v", dst), ("a", a), ("a", b), cc))
+    return out
+
+
+def dkdv_mfmas(cfg, c, first=False):
+    """dV^T[c][b] += dO^T P[c], dK^T[c][b] += Q^T dS[c]; the k-th MFMA takes trop ring slot k % 8"""
+    out = []
+    for k in range(16):
+        tensor, b, qb, s = trop_frag(cfg, k)
+        acc = cfg.dV(c, b) if tensor == 0 else cfg.dK(c, b)
+        src = cfg.S(c, qb, 8 * s) if tensor == 0 else cfg.dP(c, qb, 8 * s)
+        z = first and qb == 0 and s == 0
+        out.append(mfma(cfg, ("a", acc), ("v", cfg.tr(k % 8)), ("v", src), ("a", acc), c_is_zero=z))
+    return out
+
+
+# ---- VALU ---------------------------------------------------------------------------------
+def pds_part(cfg, c, qb):
+    """P = exp2(S) and dS = P * dP' of query block qb of chain c, packed in place"""
+    out = []
+    for s in range(2):
+        g0 = 8 * s
+        for i in range(g0, g0 + 8):
+            r = cfg.S(c, qb, i)
+            out.append(valu(f"v_exp_f32 v{r}, v{r}", [f"v{r}"], [f"v{r}"], kind="exp"))
+        for i in range(g0, g0 + 8):
+            r, d = cfg.S(c, qb, i), cfg.dP(c, qb, i)
+            out.append(valu(f"v_mul_f32 v{d}, v{d}, v{r}", [f"v{d}", f"v{r}"], [f"v{d}"]))
+        for base in (cfg.S(c, qb, g0), cfg.dP(c, qb, g0)):
+            for ii in range(4):
+                d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
+                out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
+    return tagged("sm", out)
+
+
+# ---- staging --------------------------------------------------------------------------
+def staging_loads(cfg):
+    out = []
+    for tensor, rs in ((0, "%[rsq]"), (1, "%[rsd]")):
+        for cc in range(cfg.CPT):
+            base = cfg.stg(tensor, cc)
+            for h in range(2):
+                off = f" offset:{16 * h}" if h else ""
+                out.append(Ins(f"buffer_load_dwordx4 {rtxt('v', base + 4 * h, 4)}, %[vo{cc}], {rs}, %[goff] offen{off}",
+                               "vmem", R(["s:goff"]), rng("v", base + 4 * h, 4)))
+    out.append(Ins(f"buffer_load_dword v{cfg.RCV}, %[rvo], %[rsc], %[roff] offen", "vmem", R(["s:roff"]),
+                   [f"v{cfg.RCV}"]))
+    out.append(Ins(f"s_add_u32 %[goff], %[goff], {QT * cfg.D * 4}", "salu", R(["s:goff"]), ["s:goff", "scc"]))
+    out.append(Ins(f"s_add_u32 %[roff], %[roff], {QT * 4}", "salu", R(["s:roff"]), ["s:roff", "scc"]))
+    return tagged("stg", out)
+
+
+def staging_convert(cfg, slot):
+    out = []
+    step = 256 // (cfg.D // 8)
+    for tensor in range(2):
+        for cc in range(cfg.CPT):
+            base = cfg.stg(tensor, cc)
+            for ii in range(4):
+                d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
+                out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
+            off = slot * cfg.SLOT + tensor * cfg.TBB + cc * step * cfg.D * 2
+            out.append(Ins(f"ds_write_b128 %[lo], {rtxt('v', base, 4)} offset:{off}", "dsw", R(rng("v", base, 4)), []))
+    r = cfg.RCV
+    out.append(valu(f"v_mul_f32 v{r}, %[rsm], v{r}", [f"v{r}"], [f"v{r}"]))
+    out.append(Ins(f"ds_write_b32 %[rcw], v{r} offset:{slot * cfg.SLOT + cfg.RC}", "dsw", R([f"v{r}"]), []))
+    return tagged("stg", out)
+
+
+# ---- program ---------------------------------------------------------------------------
+def body(cfg, j3, log):
+    """one 64-query step j with j % 3 == j3: its tiles in slot j3; step j+1 staged into (j3+1)%3;
+    chain B's dV/dK of step j-1 read slot (j3+2)%3"""
+    s, n, pv = j3, (j3 + 1) % 3, (j3 + 2) % 3
+    seq = []
+    # P1: S, dP of A | P, dS of B (j-1) qb 1; seeds qb 1; stage step j+1; trop 0..7 for P2
+    sd = seed_reads(cfg, s, 0, 1, 0, earliest=2, deadline=5) + seed_reads(cfg, s, 1, 1, 1, earliest=6, deadline=9)
+    pre = []
+    for k in range(8):
+        pre += trop_reads(cfg, pv, k, earliest=8)
+    conv = staging_convert(cfg, n)
+    for i in conv:
+        i.earliest = 2
+    seq += schedule_phase(cfg, sdp_mfmas(cfg, 0), [pds_part(cfg, 1, 1), sd, conv, pre], f"P1.{j3}", log)
+    # P2: dV, dK of B (j-1) | P, dS of A qb 0; trop 8..15; seeds qb 0 for P3; loads of step j+2
+    tr = []
+    for k in range(8, 16):
+        tr += trop_reads(cfg, pv, k, earliest=k - 8 + 2, deadline=k - 3)
+    sd = seed_reads(cfg, s, 0, 0, 0) + seed_reads(cfg, s, 1, 0, 1)
+    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 1), [pds_part(cfg, 0, 0), tr, sd, staging_loads(cfg)], f"P2.{j3}",
+                          log)
+    # P3: S, dP of B | P, dS of A qb 1; seeds qb 1; trop 0..7 for P4
+    sd = seed_reads(cfg, s, 0, 1, 0, earliest=2, deadline=5) + seed_reads(cfg, s, 1, 1, 1, earliest=6, deadline=9)
+    pre = []
+    for k in range(8):
+        pre += trop_reads(cfg, s, k, earliest=8)
+    seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [pds_part(cfg, 0, 1), sd, pre], f"P3.{j3}", log)
+    seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
+    seq.append(tagged("bar", [Ins("s_barrier", "bar")])[0])
+    # P4: dV, dK of A | P, dS of B qb 0; trop 8..15; Q/dO rows and seeds qb 0 of step j+1
+    tr = []
+    for k in range(8, 16):
+        tr += trop_reads(cfg, s, k, earliest=k - 8 + 2, deadline=k - 3)
+    nxt = rowop_reads(cfg, n) + seed_reads(cfg, n, 0, 0, 0) + seed_reads(cfg, n, 1, 0, 1)
+    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 0), [pds_part(cfg, 1, 0), tr, nxt], f"P4.{j3}", log)
+    return seq
+
+
+def prologue(cfg):
+    """step 0 serially (both chains' S, dP; A's P, dS and dV, dK; B's first half), step 1 staged"""
+    D, NTQ = cfg.D, cfg.NTQ
+    seq = [valu(f"v_accvgpr_write_b32 a{cfg.dK(1, 0) + i}, 0", [], [f"a{cfg.dK(1, 0) + i}"]) for i in range(32)]
+    seq += [valu(f"v_accvgpr_write_b32 a{cfg.dV(1, 0) + i}, 0", [], [f"a{cfg.dV(1, 0) + i}"]) for i in range(32)]
+    seq += staging_loads(cfg)  # step 1
+    # K and V fragments of both chains from the workgroup's K / V blocks (%[kvb]: this wave's rows)
+    for t in range(NTQ):
+        seq.append(valu(f"v_add_u32 v{t}, %[kvb], %[ka{t}]", [], [f"v{t}"]))
+    for c in range(2):
+        for t in range(NTQ):
+            seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.Kf(c, t), 4)}, v{t} offset:{c * 32 * D * 2}", "dsr",
+                           R([f"v{t}"]), rng("a", cfg.Kf(c, t), 4)))
+            seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.Vf(c, t), 4)}, v{t} offset:{KEYS * D * 2 + c * 32 * D * 2}",
+                           "dsr", R([f"v{t}"]), rng("a", cfg.Vf(c, t), 4)))
+    seq += rowop_reads(cfg, 0)
+    for c in range(2):
+        for which, qb, k in SEED_ORDER:
+            seq += seed_reads(cfg, 0, which, qb, k)
+            for t in range(NTQ):
+                if which == 0:
+                    dst, a, b = cfg.S(c, qb), cfg.Qr(qb, t), cfg.Kf(c, t)
+                else:
+                    dst, a, b = cfg.dP(c, qb), cfg.dOr(qb, t), cfg.Vf(c, t)
+                cc = ("v", cfg.seed(k)) if t == 0 else ("v", dst)
+                seq.append(mfma(cfg, ("v", dst), ("a", a), ("a", b), cc))
+    seq += pds_part(cfg, 0, 0) + pds_part(cfg, 0, 1) + pds_part(cfg, 1, 0)
+    mf = dkdv_mfmas(cfg, 0, first=True)
+    for k in range(16):
+        seq += trop_reads(cfg, 0, k)
+        seq.append(mf[k])
+    seq += staging_convert(cfg, 1)
+    seq += staging_loads(cfg)  # step 2
+    seq += [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_barrier", "bar")]
+    seq += rowop_reads(cfg, 1) + seed_reads(cfg, 1, 0, 0, 0) + seed_reads(cfg, 1, 1, 0, 1)
+    return seq
+
+
+def epilogue(cfg, last_slot_expr):
+    """after the last step: B's second half, its dV, dK; stage dK^T, dV^T (last slot: the body
+    that exits passes its slot)"""
+    seq = [Ins("s_waitcnt vmcnt(0) lgkmcnt(0)", "wait")]
+    seq += pds_part(cfg, 1, 1)
+    mf = dkdv_mfmas(cfg, 1)
+    for k in range(16):
+        seq += trop_reads(cfg, last_slot_expr, k)
+        seq.append(mf[k])
+    seq.append(Ins("s_barrier", "bar"))
+    for tensor, op in ((0, "%[oak]"), (1, "%[oav]")):
+        for c in range(2):
+            for b in range(cfg.NB):
+                for g in range(4):
+                    r = (cfg.dK(c, b) if tensor == 0 else cfg.dV(c, b)) + 4 * g
+                    off = (c * 32 * cfg.OST + 32 * b + 8 * g) * 4
+                    seq.append(Ins(f"ds_write_b128 {op}, {rtxt('a', r, 4)} offset:{off}", "dsw", R(rng("a", r, 4)), []))
+    seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
+    return seq
+
+
+def build(cfg):
+    log = [f"dK/dV D={cfg.D} {'bf16' if cfg.bf16 else 'fp16'}: {cfg.nvgpr} VGPRs + {cfg.nagpr} AGPRs in asm, "
+           f"LDS {cfg.lds_bytes} B"]
+    pro = prologue(cfg)
+    bodies = [body(cfg, j3, log) for j3 in (1, 2, 0)]
+    empty = ((), ())
+    pro, st = insert_waits(pro, empty)
+    # the loop head is entered from the prologue and from the back edge: iterate the set of
+    # possible wait states there to a fixed point, waits valid for all of them
+    heads = [st]
+    for _ in range(8):
+        done, cur = [], heads
+        for b in bodies:
+            b2, cur = insert_waits_multi(b, cur)
+            done.append(b2)
+        new = [x for x in cur if x not in heads]
+        if not new:
+            break
+        heads = heads + new
+    else:
+        raise AssertionError("loop-carried wait states do not converge")
+    # three epilogues: the last step's slot is that of the body that exits
+    epis = []
+    for j3 in (1, 2, 0):
+        e, _ = insert_waits(epilogue(cfg, j3), empty)
+        epis.append(e)
+    ctl = lambda lab, cmp: [Ins("s_sub_u32 %[cnt], %[cnt], 1", "salu", R(["s:cnt"]), ["s:cnt", "scc"]),
+                            Ins(f"{cmp} %[cnt], 0", "salu", R(["s:cnt"]), ["scc"]),
+                            Ins(f"s_cbranch_scc1 {lab}", "branch", R(["scc"]))]
+    done[0] += ctl("FA2DK_EPI1_%=", "s_cmp_eq_u32")
+    done[1] += ctl("FA2DK_EPI2_%=", "s_cmp_eq_u32")
+    done[2] += ctl("FA2DK_LOOP_%=", "s_cmp_lg_u32") + [Ins("s_branch FA2DK_EPI0_%=", "branch")]
+    for _ in range(3):
+        pro = fix_hazards(pro, [[]])
+        done[0] = fix_hazards(done[0], [pro[-40:], done[2][-40:]])
+        done[1] = fix_hazards(done[1], [done[0][-40:]])
+        done[2] = fix_hazards(done[2], [done[1][-40:]])
+        for k in range(3):
+            epis[k] = fix_hazards(epis[k], [done[k][-40:]])
+    lines = [i.text for i in pro] + ["FA2DK_LOOP_%=:"]
+    for k in range(3):
+        lines += [i.text for i in done[k]]
+    for k, lab in enumerate(("FA2DK_EPI1_%=", "FA2DK_EPI2_%=", "FA2DK_EPI0_%=")):
+        lines += [lab + ":"] + [i.text for i in epis[k]]
+        if k < 2:
+            lines.append("s_branch FA2DK_END_%=")
+    lines.append("FA2DK_END_%=:")
+    allb = done[0] + done[1] + done[2]
+    nm = sum(1 for i in allb if i.kind == "mfma")
+    nv = sum(1 for i in allb if i.kind in ("valu", "exp"))
+    nn = sum(int(i.text.split()[1]) + 1 for i in allb if i.kind == "nop")
+    log.append(f"  loop (3 steps): {nm} MFMA, {nv} VALU ({nv / nm:.2f} per MFMA), {nn} nop wait states, "
+               f"{len(allb)} instructions")
+    return lines, log
+
+
+def operands(cfg):
+    outs = ['[cnt] "+s"(hs_cnt)', '[goff] "+s"(hs_goff)', '[roff] "+s"(hs_roff)']
+    ins = [f'[ka{t}] "v"(hs_ka[{t}])' for t in range(cfg.NTQ)]
+    ins += [f'[tr{b}_{k}] "v"(hs_tr[{b}][{k}])' for b in range(cfg.NB) for k in range(2)]
+    ins += [f'[vo{c}] "v"(hs_vo[{c}])' for c in range(cfg.CPT)]
+    ins += ['[lo] "v"(hs_lo)', '[rco] "v"(hs_rco)', '[rvo] "v"(hs_rvo)', '[rcw] "v"(hs_rcw)', '[oak] "v"(hs_oak)',
+            '[oav] "v"(hs_oav)', '[rsq] "s"(hs_rsq)', '[rsd] "s"(hs_rsd)', '[rsc] "s"(hs_rsc)', '[rsm] "s"(hs_rsm)',
+            '[kvb] "s"(hs_kvb)']
+    clob = [f'"v{i}"' for i in range(cfg.nvgpr)] + [f'"a{i}"' for i in range(cfg.nagpr)] + ['"vcc"', '"scc"', '"memory"']
+    return outs, ins, clob
+
+
+def emit():
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = ["// Generated by cuda-flash-attention_amd/gen/gen_bwd_dkdv.py -- do not edit.",
+           "// Hand-scheduled dK/dV loop of fa2_bwd_dkdv_hs_kernel<D> (f-attn2-backward_f16.cu).",
+           "#pragma once", ""]
+    logs = []
+    for bf16 in (False, True):
+        cfg = Cfg(64, bf16)
+        lines, log = build(cfg)
+        logs += log
+        out.append(f"#define FA2_DK_ASM_D64_{'BF16' if bf16 else 'F16'} \\")
+        out += [f'    "{ln}\\n\\t" \\' for ln in lines]
+        out.append('    ""')
+        out.append("")
+    cfg = Cfg(64, False)
+    o, i, c = operands(cfg)
+    out.append("#define FA2_DK_OUTPUTS_D64 " + ", ".join(o))
+    out.append("#define FA2_DK_INPUTS_D64 " + ", ".join(i))
+    out.append("#define FA2_DK_CLOBBERS_D64 " + ", ".join(c))
+    out.append(f"#define FA2_DK_LDS_D64 {cfg.lds_bytes}")
+    out.append(f"#define FA2_DK_SLOT_D64 {cfg.SLOT}")
+    out.append(f"#define FA2_DK_RC_D64 {cfg.RC}")
+    out.append(f"#define FA2_DK_KVB_D64 {cfg.KVB}")
+    out.append("")
+    out = ["// " + ln for ln in logs] + out
+    text = "\n".join(out) + "\n"
+    path = os.path.join(here, "..", "kernels", "fa2_bwd_dkdv_hs.inc")
+    if "--check" in sys.argv:
+        cur = open(path).read() if os.path.exists(path) else ""
+        if cur != text:
+            print("fa2_bwd_dkdv_hs.inc is stale: run gen/gen_bwd_dkdv.py")
+            sys.exit(1)
+        return
+    with open(path, "w") as f:
+        f.write(text)
+    print("\n".join(logs))
+
+
+if __name__ == "__main__":
+    emit()

@@ -1618,6 +1618,119 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
         if (qrow0 + row < S) *reinterpret_cast<f32x4*>(dQ + base + (long)(qrow0 + row) * D + c4) = v;
     }
 }
+// ---------------------------------------------------------------------------
+// Hand-scheduled dK/dV (D = 64; S % 64 == 0, S >= 128), r05.
+// ---------------------------------------------------------------------------
+// One workgroup = 4 waves = 256 keys, one wave per SIMD; each wave keeps 64 keys as two
+// 32-key chains (K, V fragments and dKᵀ / dVᵀ accumulators in AGPRs) while the head's
+// queries stream in 64-row steps (Q, dO tiles and the -LSE·log2e / -Δ rows) through a
+// 3-slot LDS ring.  Per step four MFMA phases alternate the chains: S and dP of one chain
+// while the other chain's P and dS are formed in the MFMA gaps, then that chain's
+// dVᵀ += dOᵀ P and dKᵀ += Qᵀ dS.  The loop is the generated inline-asm block of
+// fa2_bwd_dkdv_hs.inc (gen/gen_bwd_dkdv.py).  This kernel stages the K block (scaled by
+// log2(e)/sqrt(D)) and the V block for the asm's fragment reads, the first step's tiles
+// and row constants, and hands every wave the same staging code: wave 0 loads the next
+// step's LSE row, wave 1 its Δ row, waves 2 and 3 a null descriptor into a sink.  dK and
+// dV leave through an LDS stage as whole rows (dK times 1/sqrt(D)); every element is
+// summed in one fixed order (the reference: f-attn2-backward_f16.cu:170-268).
+}  // namespace fa2f16b
+#include "fa2_bwd_dkdv_hs.inc"
+namespace fa2f16b {
+
+template <int D>
+__global__ void __launch_bounds__(256, 1)
+fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+                       const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
+                       float* __restrict__ dK, float* __restrict__ dV, int S) {
+    static_assert(D == 64, "hand-scheduled dK/dV: D = 64");
+    constexpr int TB = 64 * D, OST = D + 4;
+    constexpr int SLOT = FA2_DK_SLOT_D64, RC = FA2_DK_RC_D64, KVB = FA2_DK_KVB_D64;
+    __shared__ __attribute__((aligned(16))) char lds[FA2_DK_LDS_D64];
+    _Float16* sh = reinterpret_cast<_Float16*>(lds);
+
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nkb = (S + 255) / 256;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = bid / nkb, kblk = bid - bh * nkb;
+    const long base = (long)bh * S * D;
+    const long rbase = (long)bh * S;
+    const int krow0 = kblk * 256;
+
+    // K block (scaled) and V block -> LDS [KVB, KVB + 2 * 256 * D * 2) bytes
+    {
+        TileStager<D, 256, 256> kst;
+        kst.init(K + base, S, tid);
+        kst.load(krow0);
+        kst.store(sh + KVB / 2, FA2B_LOG2E / __builtin_sqrtf((float)D), tid);
+    }
+    {
+        TileStager<D, 256, 256> vst;
+        vst.init(V + base, S, tid);
+        vst.load(krow0);
+        vst.store(sh + KVB / 2 + 256 * D, 1.f, tid);
+    }
+    // step 0: Q, dO tiles and the row constants -> slot 0
+    TileStager<D, 64, 256> qs, ds;
+    qs.init(Q + base, S, tid);
+    ds.init(dO + base, S, tid);
+    qs.load(0);
+    ds.load(0);
+    qs.store(sh, 1.f, tid);
+    ds.store(sh + TB, 1.f, tid);
+    if (tid < 64) {
+        float* rc = reinterpret_cast<float*>(lds + RC);
+        rc[tid] = tid < S ? -LSE[rbase + tid] * FA2B_LOG2E : 0.f;
+        rc[64 + tid] = tid < S ? -Delta[rbase + tid] : 0.f;
+    }
+    __syncthreads();
+
+    FragOffsets<D> fo;
+    fo.init(lane);
+    int hs_ka[D / 16], hs_tr[D / 32][2], hs_vo[D / 32];
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) hs_ka[t] = fo.row[t] * 2;
+#pragma unroll
+    for (int b = 0; b < D / 32; ++b) {
+        hs_tr[b][0] = fo.tr[b][0] * 2;
+        hs_tr[b][1] = fo.tr[b][1] * 2;
+    }
+#pragma unroll
+    for (int c = 0; c < D / 32; ++c) hs_vo[c] = qs.voff[c];
+    const int hs_lo = qs.loff[0] * 2;
+    const int hs_rco = 16 * h, hs_rvo = 4 * lane;
+    const int hs_rcw = (wave < 2 ? 256 * wave : 512) + 4 * lane;
+    const int hs_oak = ((wave * 64 + r) * OST + 4 * h) * 4, hs_oav = hs_oak + 256 * OST * 4;
+    const __amdgpu_buffer_rsrc_t hs_rsq = qs.rs, hs_rsd = ds.rs;
+    // the row-constant stream of this wave: LSE (wave 0), Δ (wave 1), nothing (num_records 0)
+    const __amdgpu_buffer_rsrc_t hs_rsc = head_rsrc(wave == 1 ? Delta + rbase : LSE + rbase, wave < 2 ? S : 0, 1);
+    const float hs_rsm = __builtin_bit_cast(
+        float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, wave == 0 ? -FA2B_LOG2E : wave == 1 ? -1.f : 0.f)));
+    const int hs_kvb = __builtin_amdgcn_readfirstlane(KVB + wave * 64 * D * 2);
+    int hs_cnt = __builtin_amdgcn_readfirstlane(S / 64 - 1);
+    int hs_goff = __builtin_amdgcn_readfirstlane(64 * D * 4);
+    int hs_roff = __builtin_amdgcn_readfirstlane(64 * 4);
+    (void)SLOT;
+#ifdef FA2_TILE_BF16
+    asm volatile(FA2_DK_ASM_D64_BF16 : FA2_DK_OUTPUTS_D64 : FA2_DK_INPUTS_D64 : FA2_DK_CLOBBERS_D64);
+#else
+    asm volatile(FA2_DK_ASM_D64_F16 : FA2_DK_OUTPUTS_D64 : FA2_DK_INPUTS_D64 : FA2_DK_CLOBBERS_D64);
+#endif
+    // dK rows (stage at 0) and dV rows (stage at 256 * OST floats) -> HBM as whole rows
+    constexpr int LPR = D / 4, RPI = 64 / LPR;
+    const float dscale = 1.f / __builtin_sqrtf((float)D);
+    const float* os = reinterpret_cast<const float*>(lds);
+#pragma unroll 4
+    for (int rr = 0; rr < 64; rr += RPI) {
+        const int row = wave * 64 + rr + lane / LPR, c4 = (lane % LPR) * 4;
+        const f32x4 vk = *reinterpret_cast<const f32x4*>(os + row * OST + c4) * dscale;
+        const f32x4 vv = *reinterpret_cast<const f32x4*>(os + (256 + row) * OST + c4);
+        if (krow0 + row < S) {
+            *reinterpret_cast<f32x4*>(dK + base + (long)(krow0 + row) * D + c4) = vk;
+            *reinterpret_cast<f32x4*>(dV + base + (long)(krow0 + row) * D + c4) = vv;
+        }
+    }
+}
 #endif  // CUPY_INLINE_COMPILE
 
 template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1, bool PIPE = false>
@@ -1919,6 +2032,21 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     // 4-tile staging registers spill).  Measured (B2_H8_D64, r01): S = 512 16.1 -> 12.1
     // us, 1024 29.1 -> 20.8, 2048 53.7 -> 44.3.
     int qs = tune_knob("DKDV_QS", 0);
+    if constexpr (D == 64) {
+        // hand-scheduled kernel (r05): whole 64-query steps, and a grid of at least one
+        // 256-key workgroup per CU.  DKDV_HS (tests and tools): 1 forces it (an error where
+        // it cannot serve), 0 disables it
+        const int hs = tune_knob("DKDV_HS", -1);
+        const bool fits = S % 64 == 0 && S >= 128;
+        if (hs == 1 && !fits) return hipErrorInvalidValue;
+        const long hgrid = (long)bh * ((S + 255) / 256);
+        if (fits && (hs == 1 || (hs < 0 && nw == 0 && qs == 0 && hgrid >= cu_count()))) {
+            if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_hs_kernel<D>), dim3((unsigned)hgrid), dim3(256), 0, stream, q, k,
+                               v, dout, lse, delta, dk, dv, S);
+            return hipGetLastError();
+        }
+    }
     if (qs == 0 && nw == 0 && D <= 64) {
         const int a = auto_waves(units, 8);
         if (a == 4) qs = 2, nw = 8;

@@ -1,11 +1,12 @@
 """GPU parity of the hand-scheduled backward kernels (r05) against the oracle.
 
 fa2_bwd_dq_hs_kernel<64> (generated asm loop, gen/gen_bwd_dq.py) computes dQ (and Δ, when
-it gets O) for D = 64 on whole 64-key tiles; it is the default dQ launch wherever its grid
-holds at least one 256-row workgroup per CU (C3, C5, the S = 4096 sweep point).  DQ_HS = 1
-forces it onto the small shapes here: one and several 256-row blocks per head, a last
-block with rows past S, N(0,1) inputs and gradients, both tile types, Δ fused (O given)
-and Δ supplied.  Tolerances are the north star's (1e-2 fp16, 2e-2 bf16, gradients scaled
+it gets O) and fa2_bwd_dkdv_hs_kernel<64> (gen/gen_bwd_dkdv.py) dK and dV, for D = 64 on
+whole 64-row tiles; each is the default launch wherever its grid holds at least one
+256-row workgroup per CU (C3, C5, the S = 4096 sweep point).  DQ_HS = 1 / DKDV_HS = 1 force
+them onto the small shapes here: one and several 256-row blocks per head, a last block
+with rows past S, every exit of the dK/dV loop's three-step unroll, N(0,1) inputs and
+gradients, both tile types, Δ fused (O given) and Δ supplied.  Tolerances are the north star's (1e-2 fp16, 2e-2 bf16, gradients scaled
 by max(1, max|ref|) as in test_gpu_parity.py).
 """
 import numpy as np
@@ -54,11 +55,17 @@ def _case(shape, seed=3, gauss=False):
     return (q, k, v, do, eo.astype(np.float32), el.astype(np.float32)), (edq, edk, edv, edl)
 
 
+HS_KNOBS = [{"DQ_HS": 1, "DKDV_HS": 0}, {"DQ_HS": 0, "DKDV_HS": 1}, {"DQ_HS": 1, "DKDV_HS": 1}]
+
+
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-@pytest.mark.parametrize("shape", DQ_SHAPES, ids=lambda s: "B%d_H%d_S%d_D%d" % s)
-def test_hs_dq_full_backward(shape, precision):
-    """fa2_backward's two-kernel plan with the hand-scheduled dQ (Δ fused, written out for dK/dV)"""
-    fa2amd.tune_set("DQ_HS", 1)
+@pytest.mark.parametrize("knobs", HS_KNOBS, ids=["dq_hs", "dkdv_hs", "both_hs"])
+@pytest.mark.parametrize("shape", DQ_SHAPES + [(1, 1, 384, 64), (1, 1, 448, 64)], ids=lambda s: "B%d_H%d_S%d_D%d" % s)
+def test_hs_full_backward(shape, knobs, precision):
+    """fa2_backward's two-kernel plan with the hand-scheduled dQ (Δ fused, written out for
+    dK/dV) and / or the hand-scheduled dK/dV"""
+    for key, val in knobs.items():
+        fa2amd.tune_set(key, val)
     fa2amd.tune_set("BWD_FUSED", 0)
     (q, k, v, do, o, lse), (edq, edk, edv, _) = _case(shape)
     tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
@@ -89,6 +96,40 @@ def test_hs_dq_entry_points(shape, fused_delta):
     assert maxerr(dq.cpu().numpy(), edq) < TOL["fp16"] * max(1.0, float(np.abs(edq).max()))
 
 
+def test_hs_dkdv_entry_point():
+    """fa2_backward_dkdv (Δ supplied) through the hand-scheduled kernel"""
+    fa2amd.tune_set("DKDV_HS", 1)
+    (q, k, v, do, o, lse), (_, edk, edv, edl) = _case((2, 2, 1024, 64), seed=5, gauss=True)
+    tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
+    dl = fa2amd.delta(tdo, to)
+    dk, dv = torch.empty_like(tq), torch.empty_like(tq)
+    fa2amd.backward_dkdv(tq, tk, tv, tdo, tl, dl, dk, dv)
+    torch.cuda.synchronize()
+    for got, exp in ((dk, edk), (dv, edv)):
+        assert maxerr(got.cpu().numpy(), exp) < TOL["fp16"] * max(1.0, float(np.abs(exp).max()))
+
+
+def test_hs_dkdv_deterministic_and_default():
+    """bitwise repeatable; at C3's grid the default dK/dV launch is the hand-scheduled one"""
+    B, H, S, D = 4, 16, 2048, 64
+    q, k, v = fo.harness_inputs(B, H, S, D, seed=4)
+    do = np.random.RandomState(10).randn(B, H, S, D).astype(np.float32)
+    tq, tk, tv, tdo = cuda(q, k, v, do)
+    o, lse = fa2amd.forward(tq, tk, tv, "fp16")
+    res = []
+    for hs in (-1, 1, 1, 0):
+        fa2amd.tune_set("DKDV_HS", hs)
+        dq, dk, dv = fa2amd.backward(tq, tk, tv, o, tdo, lse, "fp16")
+        torch.cuda.synchronize()
+        res.append((dk.cpu().numpy(), dv.cpu().numpy()))
+    for t in range(2):
+        assert np.array_equal(res[0][t], res[1][t]) and np.array_equal(res[1][t], res[2][t])
+        assert maxerr(res[1][t], res[3][t]) < 2e-3 * max(1.0, float(np.abs(res[3][t]).max()))
+    _, edk, edv, _ = fo.attention_backward(q[:1, :2], k[:1, :2], v[:1, :2], do[:1, :2])
+    assert maxerr(res[1][0][:1, :2], edk) < TOL["fp16"] * max(1.0, float(np.abs(edk).max()))
+    assert maxerr(res[1][1][:1, :2], edv) < TOL["fp16"] * max(1.0, float(np.abs(edv).max()))
+
+
 def test_hs_dq_deterministic_and_default():
     """bitwise repeatable; at C3's grid the default dQ launch is the hand-scheduled one"""
     B, H, S, D = 4, 16, 2048, 64
@@ -108,9 +149,10 @@ def test_hs_dq_deterministic_and_default():
     assert maxerr(res[1][:1, :2], edq) < TOL["fp16"] * max(1.0, float(np.abs(edq).max()))
 
 
+@pytest.mark.parametrize("knob", ["DQ_HS", "DKDV_HS"])
 @pytest.mark.parametrize("shape", [(1, 1, 100, 64), (1, 1, 64, 64)])
-def test_hs_dq_forced_on_unserved_shape_is_an_error(shape):
-    fa2amd.tune_set("DQ_HS", 1)
+def test_hs_bwd_forced_on_unserved_shape_is_an_error(shape, knob):
+    fa2amd.tune_set(knob, 1)
     fa2amd.tune_set("BWD_FUSED", 0)
     (q, k, v, do, o, lse), _ = _case(shape)
     tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
