@@ -233,3 +233,34 @@ def fix_hazards(block, preds):
             need -= k
         out.append(ins)
     return out
+
+
+ABL = set()  # timing-only ablations (--abl a,b --out file): results are invalid, never the product .inc
+
+
+def ablate(seq):
+    """drop the loop-body instructions the active ablations name"""
+    if not ABL:
+        return seq
+    out = []
+    for i in seq:
+        if i.tag == "flag":
+            continue
+        if ("nobar" in ABL and i.kind == "bar") or ("nostage" in ABL and i.tag == "stg") or \
+                ("nolds" in ABL and i.tag == "lds") or ("nosm" in ABL and i.tag == "sm") or \
+                ("noexp" in ABL and i.kind == "exp") or ("nomfma" in ABL and i.kind == "mfma") or \
+                ("nowait" in ABL and i.kind == "wait"):
+            continue
+        out.append(i)
+    return out
+
+
+def parse_abl(argv):
+    if "--abl" in argv:
+        ABL.update(argv[argv.index("--abl") + 1].split(","))
+        assert "--out" in argv, "ablation builds write elsewhere (--out): never the product .inc"
+
+
+def ablate_waits(seq):
+    """the 'nowait' ablation: no counted waits inside the loop bodies (a timing probe only)"""
+    return [i for i in seq if not ("nowait" in ABL and i.kind == "wait")] if ABL else seq

@@ -38,7 +38,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from asmgen import Ins, R, fix_hazards, insert_waits, insert_waits_multi, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402,E501
+import asmgen  # noqa: E402
+from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, insert_waits_multi, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402,E501
 
 QT = 64  # queries per step
 KEYS = 256  # keys per workgroup
@@ -343,7 +344,7 @@ def build(cfg):
     log = [f"dK/dV D={cfg.D} {'bf16' if cfg.bf16 else 'fp16'}: {cfg.nvgpr} VGPRs + {cfg.nagpr} AGPRs in asm, "
            f"LDS {cfg.lds_bytes} B"]
     pro = prologue(cfg)
-    bodies = [body(cfg, j3, log) for j3 in (1, 2, 0)]
+    bodies = [ablate(body(cfg, j3, log)) for j3 in (1, 2, 0)]
     empty = ((), ())
     pro, st = insert_waits(pro, empty)
     # the loop head is entered from the prologue and from the back edge: iterate the set of
@@ -355,11 +356,12 @@ def build(cfg):
             b2, cur = insert_waits_multi(b, cur)
             done.append(b2)
         new = [x for x in cur if x not in heads]
-        if not new:
+        if not new or asmgen.ABL:
             break
         heads = heads + new
     else:
         raise AssertionError("loop-carried wait states do not converge")
+    done = [ablate_waits(b) for b in done]
     # three epilogues: the last step's slot is that of the body that exits
     epis = []
     for j3 in (1, 2, 0):
@@ -390,7 +392,7 @@ def build(cfg):
     nm = sum(1 for i in allb if i.kind == "mfma")
     nv = sum(1 for i in allb if i.kind in ("valu", "exp"))
     nn = sum(int(i.text.split()[1]) + 1 for i in allb if i.kind == "nop")
-    log.append(f"  loop (3 steps): {nm} MFMA, {nv} VALU ({nv / nm:.2f} per MFMA), {nn} nop wait states, "
+    log.append(f"  loop (3 steps): {nm} MFMA, {nv} VALU ({nv / max(nm, 1):.2f} per MFMA), {nn} nop wait states, "
                f"{len(allb)} instructions")
     return lines, log
 
@@ -434,6 +436,8 @@ def emit():
     out = ["// " + ln for ln in logs] + out
     text = "\n".join(out) + "\n"
     path = os.path.join(here, "..", "kernels", "fa2_bwd_dkdv_hs.inc")
+    if "--out" in sys.argv:
+        path = sys.argv[sys.argv.index("--out") + 1]
     if "--check" in sys.argv:
         cur = open(path).read() if os.path.exists(path) else ""
         if cur != text:
@@ -446,4 +450,5 @@ def emit():
 
 
 if __name__ == "__main__":
+    asmgen.parse_abl(sys.argv)
     emit()

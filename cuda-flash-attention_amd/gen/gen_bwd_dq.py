@@ -38,7 +38,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from asmgen import Ins, R, fix_hazards, insert_waits, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402
+import asmgen  # noqa: E402
+from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402
 
 KT = 64
 ROWS = 256
@@ -295,13 +296,14 @@ def epilogue(cfg):
 def build(cfg):
     log = [f"dQ D={cfg.D} {'bf16' if cfg.bf16 else 'fp16'}: {cfg.nvgpr} VGPRs + {cfg.nagpr} AGPRs in asm, "
            f"LDS {cfg.lds_bytes} B"]
-    pro, b1, b0, epi = prologue(cfg), body(cfg, 1, log), body(cfg, 0, log), epilogue(cfg)
+    pro, b1, b0, epi = prologue(cfg), ablate(body(cfg, 1, log)), ablate(body(cfg, 0, log)), epilogue(cfg)
     empty = ((), ())
     pro, st_p = insert_waits(pro, empty)
     b1, st_1 = insert_waits(b1, st_p)
     b0, st_0 = insert_waits(b0, st_1)
-    assert st_0 == st_p, "loop-carried wait state differs between the prologue exit and the loop back edge"
+    assert asmgen.ABL or st_0 == st_p, "loop-carried wait state differs between the prologue exit and the loop back edge"
     epi, _ = insert_waits(epi, empty)
+    b1, b0 = ablate_waits(b1), ablate_waits(b0)
     b1 = b1 + [Ins("s_sub_u32 %[cnt], %[cnt], 1", "salu", R(["s:cnt"]), ["s:cnt", "scc"]),
                Ins("s_cmp_eq_u32 %[cnt], 0", "salu", R(["s:cnt"]), ["scc"]),
                Ins("s_cbranch_scc1 FA2DQ_EPI_%=", "branch", R(["scc"]))]
@@ -318,7 +320,7 @@ def build(cfg):
     nm = sum(1 for i in b1 + b0 if i.kind == "mfma")
     nv = sum(1 for i in b1 + b0 if i.kind in ("valu", "exp"))
     nn = sum(int(i.text.split()[1]) + 1 for i in b1 + b0 if i.kind == "nop")
-    log.append(f"  loop (2 tiles): {nm} MFMA, {nv} VALU ({nv / nm:.2f} per MFMA), {nn} nop wait states, "
+    log.append(f"  loop (2 tiles): {nm} MFMA, {nv} VALU ({nv / max(nm, 1):.2f} per MFMA), {nn} nop wait states, "
                f"{len(b1) + len(b0)} instructions")
     return lines, log
 
@@ -358,6 +360,8 @@ def emit():
     out = ["// " + ln for ln in logs] + out
     text = "\n".join(out) + "\n"
     path = os.path.join(here, "..", "kernels", "fa2_bwd_dq_hs.inc")
+    if "--out" in sys.argv:
+        path = sys.argv[sys.argv.index("--out") + 1]
     if "--check" in sys.argv:
         cur = open(path).read() if os.path.exists(path) else ""
         if cur != text:
@@ -370,4 +374,5 @@ def emit():
 
 
 if __name__ == "__main__":
+    asmgen.parse_abl(sys.argv)
     emit()

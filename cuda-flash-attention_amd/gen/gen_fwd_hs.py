@@ -47,7 +47,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from asmgen import Ins, R, fix_hazards, insert_waits, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402
+import asmgen  # noqa: E402
+from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402,E501
 
 KT = 64  # keys per tile
 NWAVE = 4
@@ -399,32 +400,6 @@ def epilogue(cfg):
 # ---------------------------------------------------------------------------------------
 # whole program
 # ---------------------------------------------------------------------------------------
-ABL = set()  # timing-only ablations (gen_fwd_hs.py --abl a,b --out file): results are invalid
-
-
-def ablate(seq):
-    """drop the loop-body instructions an ablation names (never in the product .inc)"""
-    if not ABL:
-        return seq
-    drop = set()
-    if "nobar" in ABL:
-        drop.add("bar")
-    if "nostage" in ABL:
-        drop.add("stg")
-    if "nolds" in ABL:
-        drop.add("lds")
-    if "nosm" in ABL:
-        drop.add("sm")
-    out = []
-    for i in seq:
-        if i.tag == "flag" or i.tag in drop or (i.kind == "bar" and "bar" in drop):
-            continue
-        if "noexp" in ABL and i.kind == "exp":
-            continue
-        out.append(i)
-    return out
-
-
 def build(cfg):
     log = [f"D={cfg.D} {'bf16' if cfg.bf16 else 'fp16'}: {cfg.nvgpr} VGPRs + {cfg.nagpr} AGPRs in asm, "
            f"LDS {cfg.lds_bytes} B"]
@@ -436,8 +411,9 @@ def build(cfg):
     pro, st_p = insert_waits(pro, empty)
     b1, st_1 = insert_waits(b1, st_p)
     b0, st_0 = insert_waits(b0, st_1)
-    assert ABL or st_0 == st_p, "loop-carried wait state differs between the prologue exit and the loop back edge"
+    assert asmgen.ABL or st_0 == st_p, "loop-carried wait state differs between the prologue exit and the loop back edge"
     epi, _ = insert_waits(epi, ((), ()))  # starts with a full drain
+    b1, b0 = ablate_waits(b1), ablate_waits(b0)
     loop_ctl1 = [Ins("s_sub_u32 %[cnt], %[cnt], 1", "salu", R(["s:cnt"]), ["s:cnt", "scc"]),
                  Ins("s_cmp_eq_u32 %[cnt], 0", "salu", R(["s:cnt"]), ["scc"]),
                  Ins("s_cbranch_scc1 FA2HS_EPI_%=", "branch", R(["scc"]))]
@@ -456,7 +432,7 @@ def build(cfg):
     nm = sum(1 for i in b1 + b0 if i.kind == "mfma")
     nv = sum(1 for i in b1 + b0 if i.kind in ("valu", "exp"))
     nn = sum(int(i.text.split()[1]) + 1 for i in b1 + b0 if i.kind == "nop")
-    log.append(f"  loop (2 tiles): {nm} MFMA, {nv} VALU ({nv / nm:.2f} per MFMA), {nn} nop wait states, "
+    log.append(f"  loop (2 tiles): {nm} MFMA, {nv} VALU ({nv / max(nm, 1):.2f} per MFMA), {nn} nop wait states, "
                f"{len(b1) + len(b0)} instructions")
     return lines, log
 
@@ -512,7 +488,5 @@ def emit():
 
 
 if __name__ == "__main__":
-    if "--abl" in sys.argv:
-        ABL.update(sys.argv[sys.argv.index("--abl") + 1].split(","))
-        assert "--out" in sys.argv, "ablation builds write elsewhere (--out): never the product .inc"
+    asmgen.parse_abl(sys.argv)
     emit()

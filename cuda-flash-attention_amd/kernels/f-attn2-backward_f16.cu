@@ -1526,7 +1526,10 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
 // rows it leaves (unscaled fp32) in an LDS stage.  Every dQ element is summed in one fixed
 // order: bitwise reproducible, no atomics (the reference: f-attn2-backward_f16.cu:240-301).
 }  // namespace fa2f16b
-#include "fa2_bwd_dq_hs.inc"
+#ifndef FA2_DQ_INC
+#define FA2_DQ_INC "fa2_bwd_dq_hs.inc"  // (timing-only ablation builds name another, tools/r05_hs_abl.sh)
+#endif
+#include FA2_DQ_INC
 namespace fa2f16b {
 
 template <int D>
@@ -1634,7 +1637,10 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
 // dV leave through an LDS stage as whole rows (dK times 1/sqrt(D)); every element is
 // summed in one fixed order (the reference: f-attn2-backward_f16.cu:170-268).
 }  // namespace fa2f16b
-#include "fa2_bwd_dkdv_hs.inc"
+#ifndef FA2_DK_INC
+#define FA2_DK_INC "fa2_bwd_dkdv_hs.inc"  // (timing-only ablation builds name another, tools/r05_hs_abl.sh)
+#endif
+#include FA2_DK_INC
 namespace fa2f16b {
 
 template <int D>
@@ -2036,7 +2042,9 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
         // hand-scheduled kernel (r05): whole 64-query steps, and a grid of at least one
         // 256-key workgroup per CU.  DKDV_HS (tests and tools): 1 forces it (an error where
         // it cannot serve), 0 disables it
-        const int hs = tune_knob("DKDV_HS", -1);
+        // (default off: at C3 it measured 145 vs 138 us for the 8-wave 16x16x32 kernel, r05
+        // in-process A/B, profiles/r05/; it stays reachable for tests and A/Bs)
+        const int hs = tune_knob("DKDV_HS", 0);
         const bool fits = S % 64 == 0 && S >= 128;
         if (hs == 1 && !fits) return hipErrorInvalidValue;
         const long hgrid = (long)bh * ((S + 255) / 256);
