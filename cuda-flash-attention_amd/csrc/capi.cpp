@@ -64,9 +64,9 @@ std::atomic<int> g_tune_n{0};
 
 // the launch-plan overrides the launchers read (fa2_tune_set rejects other names,
 // so a misspelt knob cannot silently leave an A/B on the default plan)
-const char* const kKnobs[] = {"FWD_HS", "FWD_WAVES", "FWD_KS", "FWD_NKB","DKDV_WAVES", "DKDV_QS", "DKDV_HS", "DQ_WAVES",        "DQ_KS", "DQ_HS",
-                              "BWD_FUSED", "BWD_FUSED_DELTA", "BWD_FQS", "BWD_FKS", "BWD_FNW", "DQ_PIPE", "BWD_SP", "BWD_SP_NORED",
-                              "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS"};
+const char* const kKnobs[] = {"FWD_HS",   "FWD_WAVES", "FWD_KS",          "FWD_NKB", "DKDV_WAVES", "DKDV_QS",
+                              "DKDV_HS",  "DQ_WAVES",  "DQ_KS",           "DQ_HS",   "BWD_FUSED",  "BWD_FUSED_DELTA",
+                              "BWD_FQS",  "BWD_FKS",   "BWD_FNW",         "HOST_SHARDS_ON_DEVICE0",    "HOST_CHUNKS"};
 bool known_knob(const char* k) {
     for (const char* n : kKnobs)
         if (!strcmp(n, k)) return true;
@@ -107,7 +107,7 @@ int auto_waves(long blocks32, int maxnw, int minnw) {
 
 extern "C" {
 
-int fa2_version(void) { return 1 * 10000 + 2 * 100 + 0; }
+int fa2_version(void) { return 2 * 10000 + 0 * 100 + 0; }  // 2.0: fa2_backward_ws removed
 
 #ifndef FA2_BUILD_ID
 #define FA2_BUILD_ID "unknown"
@@ -189,36 +189,6 @@ int fa2_backward(const float* q, const float* k, const float* v, const float* o,
         : precision == FA2_BF16 ? fa2::launch_backward_bf16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st)
                                 : fa2::launch_backward_f32(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S, st);
     return hip_status(e, "fa2_backward launch");
-}
-
-int fa2_backward_workspace_size(int B, int H, int S, int D, int precision, size_t* bytes) {
-    int rc;
-    if ((rc = check_shape(B, H, S, D)) || (rc = check_precision(precision))) return rc;
-    if (!bytes) return fail(FA2_E_INVALID, "null bytes pointer");
-    *bytes = precision == FA2_FP16   ? fa2::backward_workspace_bytes_f16(D, B * H, S)
-             : precision == FA2_BF16 ? fa2::backward_workspace_bytes_bf16(D, B * H, S)
-                                     : 0;
-    return FA2_OK;
-}
-
-int fa2_backward_ws(const float* q, const float* k, const float* v, const float* o, const float* dout,
-                    const float* lse, float* delta, float* dq, float* dk, float* dv, int B, int H, int S, int D,
-                    int precision, void* workspace, size_t workspace_bytes, void* stream) {
-    int rc;
-    if ((rc = check_shape(B, H, S, D)) || (rc = check_precision(precision)) ||
-        (rc = check_ptrs({q, k, v, o, dout, lse, delta, dq, dk, dv})))
-        return rc;
-    size_t need = 0;
-    if ((rc = fa2_backward_workspace_size(B, H, S, D, precision, &need))) return rc;
-    if (need == 0) return fa2_backward(q, k, v, o, dout, lse, delta, dq, dk, dv, B, H, S, D, precision, stream);
-    if (!workspace || workspace_bytes < need) return fail(FA2_E_INVALID, "workspace smaller than fa2_backward_workspace_size");
-    const hipStream_t st = static_cast<hipStream_t>(stream);
-    const hipError_t e = precision == FA2_FP16
-                             ? fa2::launch_backward_ws_f16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S,
-                                                           workspace, workspace_bytes, st)
-                             : fa2::launch_backward_ws_bf16(D, q, k, v, o, dout, lse, delta, dq, dk, dv, B * H, S,
-                                                            workspace, workspace_bytes, st);
-    return hip_status(e, "fa2_backward_ws launch");
 }
 
 int fa2_backward_dkdv(const float* q, const float* k, const float* v, const float* dout, const float* lse,

@@ -32,14 +32,14 @@ SUPPORTED_HEAD_DIMS = (32, 64, 128)
 
 # exported symbols of include/fa2_amd.h (checked by tests/test_capi_symbols.py)
 C_SYMBOLS = (
-    "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_workspace_size", "fa2_backward_ws", "fa2_backward_dkdv",
+    "fa2_forward", "fa2_delta", "fa2_backward", "fa2_backward_dkdv",
     "fa2_backward_dq", "fa2_backward_dq_delta", "fa2_naive_forward", "fa2_fa1_forward",
     "fa2_forward_host", "fa2_backward_host", "fa2_host_release", "fa2_shard_range", "fa2_tune_set", "fa2_tune_get", "fa2_last_error",
     "fa2_version", "fa2_build_id", "fa2_device_count",
 )
 # launch-plan overrides fa2_tune_set accepts (include/fa2_amd.h)
-KNOBS = ("FWD_WAVES", "FWD_KS", "FWD_NKB", "DKDV_WAVES", "DKDV_QS", "DQ_WAVES", "DQ_KS", "BWD_FUSED", "BWD_FUSED_DELTA",
-         "BWD_FQS", "BWD_FKS", "BWD_FNW", "DQ_PIPE", "BWD_SP", "BWD_SP_NORED", "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS")
+KNOBS = ("FWD_HS", "FWD_WAVES", "FWD_KS", "FWD_NKB", "DKDV_WAVES", "DKDV_QS", "DKDV_HS", "DQ_WAVES", "DQ_KS", "DQ_HS",
+         "BWD_FUSED", "BWD_FUSED_DELTA", "BWD_FQS", "BWD_FKS", "BWD_FNW", "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS")
 
 
 class FA2Error(RuntimeError):
@@ -88,8 +88,6 @@ def _load(path):
         "fa2_forward": [P] * 5 + [I] * 5 + [V],
         "fa2_delta": [P] * 3 + [I] * 4 + [V],
         "fa2_backward": [P] * 10 + [I] * 5 + [V],
-        "fa2_backward_workspace_size": [I] * 5 + [ctypes.POINTER(ctypes.c_size_t)],
-        "fa2_backward_ws": [P] * 10 + [I] * 5 + [P, ctypes.c_size_t, V],
         "fa2_backward_dkdv": [P] * 8 + [I] * 4 + [V],
         "fa2_backward_dq": [P] * 7 + [I] * 4 + [V],
         "fa2_backward_dq_delta": [P] * 8 + [I] * 4 + [V],
@@ -279,26 +277,8 @@ def backward(q, k, v, o, dout, lse, precision="fp16", dq=None, dk=None, dv=None,
     delta_buf = torch.empty((B, H, S), device=q.device, dtype=torch.float32) if delta_buf is None else delta_buf
     ptrs = _ptrs(((q, "q", 4), (k, "k", 4), (v, "v", 4), (o, "o", 4), (dout, "dout", 4), (lse, "lse", 3),
                   (delta_buf, "delta", 3), (dq, "dq", 4), (dk, "dk", 4), (dv, "dv", 4)), B, H, S, D, q.device)
-    prec = _PRECISION[precision]
-    nbytes = workspace_size(B, H, S, D, prec)
-    if nbytes:
-        # the single-pass plan's dQ parts: device scratch from torch's caching allocator,
-        # used in stream order by this call only
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=q.device)
-        _check(lib().fa2_backward_ws(*ptrs, B, H, S, D, prec, ws.data_ptr(), nbytes, _stream(stream, q.device)))
-    else:
-        _check(lib().fa2_backward(*ptrs, B, H, S, D, prec, _stream(stream, q.device)))
+    _check(lib().fa2_backward(*ptrs, B, H, S, D, _PRECISION[precision], _stream(stream, q.device)))
     return dq, dk, dv
-
-
-def workspace_size(B, H, S, D, precision="fp16"):
-    """Device bytes fa2_backward_ws needs for this shape (0: the plans of fa2_backward run)."""
-    L = lib()
-    if not hasattr(L, "fa2_backward_workspace_size"):
-        return 0  # an older build (tools/kbench.py A/B)
-    n = ctypes.c_size_t(0)
-    _check(L.fa2_backward_workspace_size(B, H, S, D, _PRECISION[precision], ctypes.byref(n)))
-    return n.value
 
 
 def backward_dkdv(q, k, v, dout, lse, delta_buf, dk, dv, stream=None):

@@ -36,12 +36,6 @@
 #define FA2_TILE_LAUNCH(x) x##_f16
 #define FA2_TILE_HOST(x) x##_fp16
 #endif
-#ifndef FA2_SP_MID
-#define FA2_SP_MID 1  // the previous step's dQ part runs after the step's staging loads are issued (0: before them)
-#endif
-#ifndef FA2_SP_ABL
-#define FA2_SP_ABL 0  // ablation builds (tools/ab_sp_parts.sh): 1 = no dQ product, 2 = no part stores
-#endif
 
 namespace fa2f16b {
 
@@ -440,15 +434,10 @@ struct FragOffsets16 {
 #ifndef FA2_IGLP_FUSED
 #define FA2_IGLP_FUSED 2
 #endif
-struct NoDsOut {
-    template <typename T>
-    __device__ __forceinline__ void operator()(int, const T&) const {}
-};
-// dsout(qb, dsf): the single-pass backward (SP) takes each 32-query half's packed dS here
-template <int D, int IGLP = -1, typename Mid, typename DsOut = NoDsOut>
+template <int D, int IGLP = -1, typename Mid>
 __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
                                             const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
-                                            int g, Mid&& mid, DsOut&& dsout = DsOut()) {
+                                            int g, Mid&& mid) {
 #ifdef FA2_IGLP_DKDV_ONCE
     if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
 #endif
@@ -494,7 +483,6 @@ __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* 
                 dsf[nb][j] = d2[0];
                 dsf[nb][j + 1] = d2[1];
             }
-        dsout(qb, dsf);
 #pragma unroll
         for (int md = 0; md < D / 16; ++md) {
             const f16x8 a_do = fo.trop(dOs, qb * 32, md), a_q = fo.trop(Qs, qb * 32, md);
@@ -541,7 +529,7 @@ __device__ __forceinline__ void store_block_rows16(float (*os)[36], const f32x4 
 // The workgroup's LDS: [buf][Q | dO][QS] fp16 tiles (or the query-split merge
 // records), [buf][-lse2 | -delta][QS] fp32 rows, the per-wave result stage.  Carved
 // from one block so the fused backward kernel can overlay it with the dQ role's.
-template <int D, int NW, int KB, int QS, int SP = 0>
+template <int D, int NW, int KB, int QS>
 struct DkdvLds {
     static constexpr int QT = 64, TILE = QT * D, NK = NW / QS;
     // query-split merge records: per wave of groups 1..QS-1, dKᵀ and dVᵀ (D floats per lane)
@@ -555,37 +543,20 @@ struct DkdvLds {
     static constexpr int SMEM = KV > SMEM0 ? KV : SMEM0;  // halves
     static constexpr int ROWS = 2 * SMEM;                 // byte offsets
     static constexpr int OSTAGE = ROWS + 2 * 2 * QS * QT * 4;
-    static constexpr int BASE = OSTAGE + NK * 32 * 36 * 4;
-    // SP (single pass): the workgroup's K block kept whole ([256 keys][D] fp16, scaled as
-    // for S), and two [256 keys][64 queries] dS images; the output stage, which only
-    // the epilogue uses (after the last dQ product), aliases them
-    static constexpr int KIMG = OSTAGE;
-    static constexpr int DSIMG = KIMG + 32 * NK * D * 2;
-    static constexpr int DSBUF = 32 * NK * QT * 2;  // bytes per dS image
-    static constexpr int BYTES = SP ? (DSIMG + 2 * DSBUF > BASE ? DSIMG + 2 * DSBUF : BASE) : BASE;
+    static constexpr int BYTES = OSTAGE + NK * 32 * 36 * 4;
 };
 
 // One workgroup of the dK/dV kernel; `bid` is its (XCD-remapped) block number over
 // the BH * ceil(S / (KPW * NK)) key blocks.
 // DEL: Δ = rowsum(dO ∘ O) of every staged step computed here from O rows staged
 // beside dO (no Delta input: the fused small-grid launch, whose dQ role writes Δ).
-// SP (single-pass backward, 1 = fp16 parts, 2 = fp32 parts; 8 waves, unsplit, D = 64):
-// the workgroup also produces its 256 keys' share of dQ.  Each 32-query half's packed dS
-// goes to an LDS image [keys][queries]; during the next step every wave computes a
-// 16-query x 32-column slice of that step's dQ part over all 256 keys (16 MFMAs, K and
-// dS by transposed reads) and stores it to `part` [key block][B*H][S][D] (fp16 or fp32);
-// fa2_bwd_sp_reduce sums the key blocks in order.  Δ is computed per
-// step from O (DEL) and written to `delta_out` by the head's key block 0.
-template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1, bool DEL = false, int IGLP = -1, int SP = 0>
+template <int D, int NW, int KB = 1, bool M16 = false, int QS = 1, bool DEL = false, int IGLP = -1>
 __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const float* __restrict__ Q,
                                           const float* __restrict__ K, const float* __restrict__ V,
                                           const float* __restrict__ dO, const float* __restrict__ LSE,
                                           const float* __restrict__ Delta, float* __restrict__ dK,
-                                          float* __restrict__ dV, int S, const float* __restrict__ O = nullptr,
-                                          void* __restrict__ part = nullptr, long part_stride = 0,
-                                          float* __restrict__ delta_out = nullptr) {
-    static_assert(!SP || (M16 && QS == 1 && KB == 1 && NW == 8 && D == 64), "single pass: C3 geometry");
-    using L = DkdvLds<D, NW, KB, QS, SP>;
+                                          float* __restrict__ dV, int S, const float* __restrict__ O = nullptr) {
+    using L = DkdvLds<D, NW, KB, QS>;
     constexpr int QT = L::QT;  // query rows per step
     constexpr int NT = 64 * NW;
     constexpr int TILE = L::TILE;
@@ -621,13 +592,12 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
     static_assert(KPW * NK <= 4 * QT, "K / V block fits the Q/dO buffers");
     const int kblock0 = kblk * KPW * NK;
     _Float16* const vblk = L::OVL ? smem + KPW * NK * D : smem;
-    _Float16* const kimg = SP ? reinterpret_cast<_Float16*>(lds + L::KIMG) : smem;  // the K block's image
     auto read_k = [&] {
         if constexpr (M16) {
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-                for (int ks = 0; ks < D / 32; ++ks) st16.kf[nb][ks] = fo16.rowop(kimg, wave * KPW + 16 * nb, ks);
+                for (int ks = 0; ks < D / 32; ++ks) st16.kf[nb][ks] = fo16.rowop(smem, wave * KPW + 16 * nb, ks);
         } else {
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb)
@@ -653,10 +623,10 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
     vst.init(V + base, S, tid);
     kst.load(kblock0);
     if constexpr (!L::OVL) {
-        kst.store(kimg, kscale, tid);
+        kst.store(smem, kscale, tid);
         __syncthreads();
         read_k();
-        if constexpr (!SP) __syncthreads();  // (SP: the K image is not overwritten)
+        __syncthreads();
     }
     vst.load(kblock0);
     if constexpr (!L::OVL) {
@@ -730,14 +700,12 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
         }
         load_rows(it * QS * QT);
     };
-    // SP: the head's key block 0 also writes Δ out (fa2_backward's `delta` contract)
-    float* const dl_out = SP && kblk == 0 ? delta_out + rbase : nullptr;
     auto store_step = [&](_Float16* qdst, _Float16* ddst, int rbuf, int step) {
         if (stg) {
             qs.store(qdst, 1.f, tid);
             dos.store(ddst, 1.f, tid);
             if constexpr (DEL)
-                delta_rows<D, QT * QS, NS, true>(dos, os, S, step * QS * QT, rows[rbuf][1], dl_out, tid);
+                delta_rows<D, QT * QS, NS, true>(dos, os, S, step * QS * QT, rows[rbuf][1], nullptr, tid);
         }
         store_rows(rbuf);
     };
@@ -763,99 +731,13 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
     if (QS > 1) fo16.shift(qg * TILE);
     const int rq = qg * QT;  // the group's row constants
 
-    // ---- SP: the dS images and the per-step dQ part
-    _Float16* const dsimg = reinterpret_cast<_Float16*>(lds + L::DSIMG);
-    // this workgroup's part slice [S][D] of `part` (rows >= S dropped by the range check)
-    constexpr int PESZ = SP == 1 ? 2 : 4;
-    const unsigned long long part_a =
-        SP ? (unsigned long long)((char*)part + ((long)kblk * part_stride + (long)bh * S * D) * PESZ) : 0ull;
-    // (readfirstlane returns int: the halves go through unsigned variables, or the low
-    // word's bit 31 would sign-extend into the high word of the base address)
-    const unsigned part_lo = __builtin_amdgcn_readfirstlane((unsigned)part_a);
-    const unsigned part_hi = __builtin_amdgcn_readfirstlane((unsigned)(part_a >> 32));
-    const __amdgpu_buffer_rsrc_t part_rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)part_hi << 32) | part_lo), (short)0,
-                                          __builtin_amdgcn_readfirstlane(S * D * PESZ), 0x00020000);
-    // this lane's rows of the dS image (its keys) and the masked-key flag of the last block
-    const int dsrow = wave * KPW + (lane & 15);
-    const bool kok0 = key0 + (lane & 15) < S, kok1 = key0 + 16 + (lane & 15) < S;
-    auto ds_write = [&](_Float16* img) {
-        // dsf[nb]: key 16 nb + (l & 15) of this wave, k-slot j <-> query 16 (j >> 2) + 4g + (j & 3)
-        // of the 32-query half qb: two 4-query runs per key, one 8-byte write each
-        return [=](int qb, const f16x8 (&dsf)[2]) {
-            if constexpr (FA2_SP_ABL == 1) return;
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                const bool ok = nb ? kok1 : kok0;
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-                    f16x4 v = {dsf[nb][4 * hh], dsf[nb][4 * hh + 1], dsf[nb][4 * hh + 2], dsf[nb][4 * hh + 3]};
-                    if (!ok) v = f16x4{0, 0, 0, 0};
-                    *reinterpret_cast<f16x4*>(img + tile_off<64>(dsrow + 16 * nb, qb * 32 + 16 * hh + 4 * g16)) = v;
-                }
-            }
-        };
-    };
-    // dQ part of step t from dS image `img`: wave w takes queries 16 (w & 3) .. +15 of the
-    // step and columns 32 (w >> 2) .. +31, summed over the block's 256 keys (8 chunks of
-    // 32 in the transposed-read key order, the same for the K and the dS operand)
-    const int pq = wave & 3, pd = wave >> 2;
-    // transposed-read offsets of the two operands (fo16.tr for columns 16 pq and 16 (2 pd + m),
-    // computed here: indexing fo16.tr by the wave number would put the array in scratch)
-    int ptr_ds[2], ptr_k[2][2];
-    {
-        const int i16 = lane & 15, qq = i16 >> 2, p4 = i16 & 3;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            ptr_ds[hh] = tile_off<64>(16 * hh + 4 * g16 + qq, 16 * pq + 4 * p4);
-#pragma unroll
-            for (int m = 0; m < 2; ++m) ptr_k[m][hh] = tile_off<D>(16 * hh + 4 * g16 + qq, 16 * (2 * pd + m) + 4 * p4);
-        }
-    }
-    auto dq_part = [&](const _Float16* img, int t) {
-        if constexpr (FA2_SP_ABL == 1) return;
-        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-        for (int c = 0; c < KPW * NK / 32; ++c) {
-            // dSᵀ[keys 32c ..][queries 16 pq + (l & 15)] and K[keys 32c ..][columns of block 2 pd + m]
-            const f16x8 b = cat4(lds_tr4(img + ptr_ds[0] + 32 * c * 64), lds_tr4(img + ptr_ds[1] + 32 * c * 64));
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-                acc[m] = mfma16(cat4(lds_tr4(kimg + ptr_k[m][0] + 32 * c * D), lds_tr4(kimg + ptr_k[m][1] + 32 * c * D)),
-                                b, acc[m]);
-        }
-        // C[d = 16 (2 pd + m) + 4g + i][query 64 t + 16 pq + (l & 15)]: 4 consecutive columns per lane
-        const int qrow = t * QT + 16 * pq + (lane & 15);
-        if constexpr (FA2_SP_ABL == 2) {
-            asm volatile("" ::"v"(acc[0]), "v"(acc[1]));
-            return;
-        }
-        // K image is K·log2e/√D; the part is dS·K/√D
-        const float sc = 1.f / FA2B_LOG2E;
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            const int voff = qrow * D + 16 * (2 * pd + m) + 4 * g16;
-            if constexpr (SP == 1) {
-                typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-                const f16x4 h = {(_Float16)(acc[m][0] * sc), (_Float16)(acc[m][1] * sc), (_Float16)(acc[m][2] * sc),
-                                 (_Float16)(acc[m][3] * sc)};
-                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), part_rs, voff * 2, 0, 0);
-            } else {
-                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[m] * sc), part_rs, voff * 4, 0, 0);
-            }
-        }
-    };
-
     // one staged step: the group's tile (the next step's loads inside it)
     auto run_step = [&](const _Float16* Qb, const _Float16* dOb, const float* r0, const float* r1, int itc,
-                        auto&& mid, auto&& dsout) {
+                        auto&& mid) {
         if constexpr (M16) {
             const bool live = QS == 1 || itc * QS + qg < nqt;  // wave-uniform
             if (!live) mid();
-            else dkdv_step16<D, IGLP>(st16, Qb, dOb, r0 + rq, r1 + rq, fo16, g16, mid, dsout);
+            else dkdv_step16<D, IGLP>(st16, Qb, dOb, r0 + rq, r1 + rq, fo16, g16, mid);
         } else {
             dkdv_step<D, KB>(st, Qb, dOb, r0, r1, fo, h, mid);
         }
@@ -863,44 +745,17 @@ __device__ __forceinline__ void dkdv_body(char* __restrict__ lds, int bid, const
     for (int it = 0; it < nsteps; it += 2) {
         {
             const bool more = it + 1 < nsteps;
-            if constexpr (SP) {
-                if (!FA2_SP_MID && it > 0) dq_part(dsimg + L::DSBUF / 2, it - 1);
-                run_step(smem, smem + QS * TILE, rows[0][0], rows[0][1], it,
-                         [&] {
-                             if (more) load_next(it + 1);
-                             if (FA2_SP_MID && it > 0) dq_part(dsimg + L::DSBUF / 2, it - 1);
-                         },
-                         ds_write(dsimg));
-            } else {
-                run_step(smem, smem + QS * TILE, rows[0][0], rows[0][1], it, [&] { if (more) load_next(it + 1); },
-                         NoDsOut());
-            }
+            run_step(smem, smem + QS * TILE, rows[0][0], rows[0][1], it, [&] { if (more) load_next(it + 1); });
             if (more) store_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, 1, it + 1);
             __syncthreads();
         }
         if (it + 1 < nsteps) {
             const bool more = it + 2 < nsteps;
-            if constexpr (SP) {
-                if (!FA2_SP_MID) dq_part(dsimg, it);
-                run_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0], rows[1][1], it + 1,
-                         [&] {
-                             if (more) load_next(it + 2);
-                             if (FA2_SP_MID) dq_part(dsimg, it);
-                         },
-                         ds_write(dsimg + L::DSBUF / 2));
-            } else {
-                run_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0], rows[1][1], it + 1,
-                         [&] { if (more) load_next(it + 2); }, NoDsOut());
-            }
+            run_step(smem + 2 * QS * TILE, smem + 3 * QS * TILE, rows[1][0], rows[1][1], it + 1,
+                     [&] { if (more) load_next(it + 2); });
             if (more) store_step(smem, smem + QS * TILE, 0, it + 2);
             __syncthreads();
         }
-    }
-    if constexpr (SP) {
-        // the last step's part (its dS image is complete: the loop ended on a barrier);
-        // then the output stage may overwrite the images
-        dq_part(dsimg + ((nsteps - 1) & 1) * (L::DSBUF / 2), nsteps - 1);
-        __syncthreads();
     }
 
     if constexpr (QS > 1) {
@@ -958,67 +813,6 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
     // the unsplit instances (full grids: C3, C5, long S) under an LLVM scheduling strategy
     dkdv_body<D, NW, KB, M16, QS, false, QS == 1 && D == 64 ? FA2_IGLP_DKDV : -1>(lds, xcd_remap(blockIdx.x, gridDim.x),
                                                                                  Q, K, V, dO, LSE, Delta, dK, dV, S);
-}
-
-// Single-pass backward (SP): dK, dV, Δ and the dQ parts of every 256-key block in one
-// launch (grid BH * ceil(S / 256), 8 waves); fa2_bwd_sp_reduce then sums the parts.
-// SPDEL: Δ computed per step from O staged beside dO (all waves stage); else Δ is read
-// from `Delta`, which a prior fa2_delta launch wrote (four waves stage, as in dK/dV)
-#ifndef FA2_SP_DEL
-#define FA2_SP_DEL 0
-#endif
-template <int SP, bool SPDEL = FA2_SP_DEL>
-__global__ void __launch_bounds__(512)
-fa2_bwd_sp_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                      const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ O,
-                      float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV, void* __restrict__ part,
-                      long part_stride, int S) {
-    __shared__ __attribute__((aligned(16))) char lds[DkdvLds<64, 8, 1, 1, SP>::BYTES];
-    dkdv_body<64, 8, 1, true, 1, SPDEL, FA2_IGLP_DKDV, SP>(lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE,
-                                                            SPDEL ? nullptr : Delta, dK, dV, S, O, part, part_stride,
-                                                            SPDEL ? Delta : nullptr);
-}
-
-// dQ[r][:] = scale * sum over key blocks kb (in order) of part[kb][r][:]; 8 columns per thread
-template <int SP>
-__global__ void __launch_bounds__(256)
-fa2_bwd_sp_reduce(const void* __restrict__ part, long part_stride, int nkb, float* __restrict__ dQ, long n8) {
-    const long stride = (long)gridDim.x * 256;
-    for (long x = (long)blockIdx.x * 256 + threadIdx.x; x < n8; x += stride) {
-        f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-        // groups of 4 key blocks: the 4 loads of a group in flight together, summed in order
-        for (int kb0 = 0; kb0 < nkb; kb0 += 4) {
-            if constexpr (SP == 1) {
-                f16x8 h[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (kb0 + u < nkb) h[u] = reinterpret_cast<const f16x8*>(part)[(kb0 + u) * (part_stride / 8) + x];
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (kb0 + u < nkb) {
-                        a += f32x4{(float)h[u][0], (float)h[u][1], (float)h[u][2], (float)h[u][3]};
-                        b += f32x4{(float)h[u][4], (float)h[u][5], (float)h[u][6], (float)h[u][7]};
-                    }
-            } else {
-                f32x4 v[4][2];
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (kb0 + u < nkb) {
-                        const f32x4* p = reinterpret_cast<const f32x4*>(part) + (kb0 + u) * (part_stride / 4) + 2 * x;
-                        v[u][0] = p[0];
-                        v[u][1] = p[1];
-                    }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (kb0 + u < nkb) {
-                        a += v[u][0];
-                        b += v[u][1];
-                    }
-            }
-        }
-        reinterpret_cast<f32x4*>(dQ)[2 * x] = a;
-        reinterpret_cast<f32x4*>(dQ)[2 * x + 1] = b;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1129,59 +923,6 @@ __device__ __forceinline__ void dq_tile16(DqState16<D>& st, const _Float16* Ks, 
         }
 }
 
-// compile-time constants passed to generic lambdas (hiprtc has no <type_traits>)
-template <int V> struct CInt { static constexpr int value = V; };
-template <bool V> struct CBool { static constexpr bool value = V; };
-
-// The two halves of dq_tile16, for the pipelined loop (PIPE below): Sᵀ / dPᵀ of one
-// 32-key half kb and its dSᵀ (packed B operands), and that half's dQᵀ product.
-template <int D, bool MASK>
-__device__ __forceinline__ void dq_sdp16(const DqState16<D>& st, const _Float16* Ks, const _Float16* Vs,
-                                         const FragOffsets16<D>& fo, int k0, int S, int g, int kb, f16x8 (&dsf)[2]) {
-    f32x4 sa[2][2], da[2][2];  // [mbl][nb]: keys k0 + 32 kb + 16 mbl + 4g + i
-#pragma unroll
-    for (int mbl = 0; mbl < 2; ++mbl)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-            sa[mbl][nb] = st.nlse2[nb];
-            da[mbl][nb] = st.ndel[nb];
-        }
-#pragma unroll
-    for (int ks = 0; ks < D / 32; ++ks)
-#pragma unroll
-        for (int mbl = 0; mbl < 2; ++mbl) {
-            const f16x8 ka = fo.rowop(Ks, 32 * kb + 16 * mbl, ks), va = fo.rowop(Vs, 32 * kb + 16 * mbl, ks);
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                sa[mbl][nb] = mfma16(ka, st.qf[nb][ks], sa[mbl][nb]);
-                da[mbl][nb] = mfma16(va, st.df[nb][ks], da[mbl][nb]);
-            }
-        }
-    if (MASK) {
-#pragma unroll
-        for (int mbl = 0; mbl < 2; ++mbl)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (k0 + 32 * kb + 16 * mbl + 4 * g + i >= S) sa[mbl][nb][i] = -__builtin_inff();
-    }
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) dsf[nb][j] = to_tile(fast_exp2(sa[j >> 2][nb][j & 3]) * da[j >> 2][nb][j & 3]);
-}
-template <int D>
-__device__ __forceinline__ void dq_prod16(DqState16<D>& st, const _Float16* Ks, const FragOffsets16<D>& fo, int kb,
-                                          const f16x8 (&dsf)[2]) {
-#pragma unroll
-    for (int md = 0; md < D / 16; ++md) {
-        const f16x8 a = fo.trop(Ks, 32 * kb, md);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) st.dqa[md][nb] = mfma16(a, dsf[nb], st.dqa[md][nb]);
-    }
-}
-
 // DELTA: Δ is computed here (from O, fused into the dO prologue) and written to
 // `Delta` for the dK/dV kernel, which then runs after this one.
 // NKB 32-key blocks per K/V tile (1 for D = 128 at 8 waves: fewer registers).
@@ -1191,10 +932,9 @@ __device__ __forceinline__ void dq_prod16(DqState16<D>& st, const _Float16* Ks, 
 // summed in LDS in group order (deterministic) and group 0 stores.
 // The workgroup's LDS: [buf][K | V][KS] tiles (at least one Q block for the coalesced
 // prologue, and the key-split merge records), the per-wave dQ stage, the block's Δ.
-template <int D, int NW, bool DELTA, int NKB, int KS, bool PIPE = false>
+template <int D, int NW, bool DELTA, int NKB, int KS>
 struct DqLds {
     static constexpr int KT = 32 * NKB, TILE = KT * D, NQ = NW / KS;
-    // PIPE: K and V tiles in 3-slot rings (tile t in slot t % 3) instead of 2 buffers
     // key-split merge records: per wave of groups 1..KS-1, dQᵀ (D / 2 floats per lane)
     static constexpr int MERGE = KS > 1 ? 2 * (KS - 1) * NQ * (D / 2) * 64 : 0;  // in halves
     // OVL: the prologue's Q and dO blocks behind the first K/V buffer, loaded together
@@ -1202,7 +942,7 @@ struct DqLds {
     // trips are exposed; on the unsplit C3 grid it measured -1.7 %)
     static constexpr bool OVL = KS > 1 || D == 128;
     static constexpr int QD = OVL ? 2 * KS * TILE + 2 * 32 * NQ * D : 32 * NQ * D;
-    static constexpr int RING = PIPE ? 6 * TILE : 4 * KS * TILE;
+    static constexpr int RING = 4 * KS * TILE;
     static constexpr int SMEM0 = RING > QD ? RING : QD;
     static constexpr int SMEM = SMEM0 > MERGE ? SMEM0 : MERGE;  // halves
     static constexpr int OSTAGE = 2 * SMEM;                     // byte offsets
@@ -1212,25 +952,14 @@ struct DqLds {
 
 // One workgroup of the dQ kernel; `bid` is its (XCD-remapped) block number over the
 // BH * ceil(S / (32 * NQ)) query blocks.
-// PIPE (unsplit 16x16x32 instances, 64-key tiles): software-pipelined tile loop.  The
-// dQᵀ product of each tile's second 32-key half runs at the start of the NEXT step,
-// beside that step's Sᵀ / dPᵀ MFMAs, and the first half's product after the second
-// half's Sᵀ / dPᵀ, so no step ends on the dependent chain exp -> cvt -> (transposed
-// K read) -> dQ MFMA that both waves of a SIMD reach together before the barrier.
-// The deferred product reads the previous tile's K, so K and V live in 3-slot rings
-// (tile t in slot t % 3: the store of tile t + 1 overwrites tile t - 2, which the
-// barrier ending step t - 1 has retired).  Same products in the same order per
-// accumulator as the unpipelined loop, so dQ is bitwise unchanged.
-template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1, int IGLP = -1,
-          bool PIPE = false>
+template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1, int IGLP = -1>
 __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const float* __restrict__ Q,
                                         const float* __restrict__ K, const float* __restrict__ V,
                                         const float* __restrict__ dO, const float* __restrict__ LSE,
                                         float* __restrict__ Delta, float* __restrict__ dQ, int S,
                                         const float* __restrict__ O) {
-    using L = DqLds<D, NW, DELTA, NKB, KS, PIPE>;
-    static_assert(!PIPE || (M16 && KS == 1 && NKB == 2 && !L::OVL), "pipelined loop: unsplit 16x16x32, 64-key tiles");
-    constexpr int V0 = PIPE ? 3 * L::TILE : KS * L::TILE;  // first V buffer / slot
+    using L = DqLds<D, NW, DELTA, NKB, KS>;
+    constexpr int V0 = KS * L::TILE;  // first V buffer
     constexpr int KT = L::KT;
     constexpr int NT = 64 * NW;
     constexpr int TILE = L::TILE;
@@ -1265,7 +994,7 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     // branches around the loads left 34 v_mov_b64 of staging-register copies there (dQ
     // +11.8 % without).  At D <= 64 the runtime flag stays: with it gone the compiler
     // schedules the mid-tile loads differently and dQ ran 4.5 % slower at C3.
-    ks.on = vs.on = (SW == NW && (D > 64 || PIPE)) || __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
+    ks.on = vs.on = (SW == NW && D > 64) || __builtin_amdgcn_readfirstlane(tid >> 6) < SW;
     const int ntiles = (S + KT - 1) / KT;
     const int last_ragged = (S % KT) ? ntiles - 1 : -1;  // the one tile that needs key masking
     const int nsteps = (ntiles + KS - 1) / KS;
@@ -1370,56 +1099,6 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
     // the group's tile within each staged image: folded into the per-lane offsets
     if (KS > 1) fo16.shift(kg * TILE);
 
-    if constexpr (PIPE) {
-        // tiles [0, nfull) unmasked in the loop, a ragged last tile after it
-        const int nfull = S / KT;
-        f16x8 dprev[2];  // dSᵀ of the previous tile's second 32-key half
-        auto kslot = [&](int sl) { return smem + sl * TILE; };
-        auto vslot = [&](int sl) { return smem + V0 + sl * TILE; };
-        // one step on tile t in slot SL; FIRST: no previous tile; MASK: the ragged tile
-        auto pstep = [&](auto SLc, auto FIRSTc, auto MASKc, int t) {
-            constexpr int SL = decltype(SLc)::value, SN = (SL + 1) % 3, SP = (SL + 2) % 3;
-            constexpr bool FIRST = decltype(FIRSTc)::value, MASK = decltype(MASKc)::value;
-            if constexpr (!FIRST) dq_prod16<D>(st16, kslot(SP), fo16, 1, dprev);
-            f16x8 d0[2];
-            dq_sdp16<D, MASK>(st16, kslot(SL), vslot(SL), fo16, t * KT, S, g16, 0, d0);
-            // the next tile's loads (past the end: out of the buffer's range, zeros)
-            ks.load((t + 1) * KT);
-            vs.load((t + 1) * KT);
-            dq_sdp16<D, MASK>(st16, kslot(SL), vslot(SL), fo16, t * KT, S, g16, 1, dprev);
-            dq_prod16<D>(st16, kslot(SL), fo16, 0, d0);
-            // slot SN held tile t - 2 (retired by the barrier that ended step t - 1);
-            // the store after the last tile writes zeros nobody reads
-            ks.store(kslot(SN), 1.f, tid);
-            vs.store(vslot(SN), 1.f, tid);
-            __syncthreads();
-        };
-        using I0 = CInt<0>;
-        using I1 = CInt<1>;
-        using I2 = CInt<2>;
-        using BT = CBool<true>;
-        using BF = CBool<false>;
-        int t = 0;
-        if (nfull > 0) {
-            pstep(I0(), BT(), BF(), 0);
-            t = 1;
-            for (; t + 3 <= nfull; t += 3) {
-                pstep(I1(), BF(), BF(), t);
-                pstep(I2(), BF(), BF(), t + 1);
-                pstep(I0(), BF(), BF(), t + 2);
-            }
-            if (t < nfull) pstep(I1(), BF(), BF(), t++);
-            if (t < nfull) pstep(I2(), BF(), BF(), t++);
-        }
-        if (t < ntiles) {  // the ragged last tile, slot t % 3
-            const int sl = t % 3;
-            if (t == 0) pstep(I0(), BT(), BT(), 0);
-            else if (sl == 0) pstep(I0(), BF(), BT(), t);
-            else if (sl == 1) pstep(I1(), BF(), BT(), t);
-            else pstep(I2(), BF(), BT(), t);
-        }
-        dq_prod16<D>(st16, kslot((ntiles - 1) % 3), fo16, 1, dprev);  // the last tile's second half
-    } else
     for (int j = 0; j < nsteps; j += 2) {
         {
             const bool more = j + 1 < nsteps;
@@ -1739,13 +1418,13 @@ fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K,
 }
 #endif  // CUPY_INLINE_COMPILE
 
-template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1, bool PIPE = false>
+template <int D, int NW, bool DELTA = false, int NKB = 2, bool M16 = false, int KS = 1>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                       const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
                       float* __restrict__ dQ, int S, const float* __restrict__ O) {
-    __shared__ __attribute__((aligned(16))) char lds[DqLds<D, NW, DELTA, NKB, KS, PIPE>::BYTES];
-    dq_body<D, NW, DELTA, NKB, M16, KS, KS == 1 && D == 64 ? FA2_IGLP_DQ : -1, PIPE>(
+    __shared__ __attribute__((aligned(16))) char lds[DqLds<D, NW, DELTA, NKB, KS>::BYTES];
+    dq_body<D, NW, DELTA, NKB, M16, KS, KS == 1 && D == 64 ? FA2_IGLP_DQ : -1>(
         lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE, Delta, dQ, S, O);
 }
 
@@ -1761,10 +1440,6 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
 // writes Δ out), the dK/dV role per step -- so the launch depends on nothing but the
 // forward's outputs: the separate Δ kernel and its launch boundary go away, at the
 // price of the dK/dV role's O reads (these grids are latency-bound, not HBM-bound).
-#ifdef FA2_STAMPS
-#define FA2_STAMP_SLOTS 65536
-__device__ unsigned long long fa2_bwd_stamp_buf[FA2_STAMP_SLOTS][4];
-#endif
 template <int D, int NW, int QS, int KS, int NKB, bool DEL = false>
 __global__ void __launch_bounds__(64 * NW)
 fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
@@ -1774,9 +1449,6 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
     constexpr int B1 = DkdvLds<D, NW, 1, QS>::BYTES, B2 = DqLds<D, NW, DEL, NKB, KS>::BYTES;
     __shared__ __attribute__((aligned(16))) char lds[B1 > B2 ? B1 : B2];
     const int b = blockIdx.x;
-#ifdef FA2_STAMPS
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-#endif
     if (b < ndk)
         // the dK/dV role with unsplit queries takes the standalone kernel's strategy
         dkdv_body<D, NW, 1, true, QS, DEL, QS == 1 && D == 64 ? FA2_IGLP_DKDV : FA2_IGLP_FUSED>(
@@ -1784,16 +1456,6 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
     else
         dq_body<D, NW, DEL, NKB, true, KS, FA2_IGLP_FUSED>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
                                                            Delta, dQ, S, O);
-#ifdef FA2_STAMPS
-    // timing-only builds: entry, every store of the workgroup complete, role
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0 && b < FA2_STAMP_SLOTS) {
-        fa2_bwd_stamp_buf[b][0] = t0;
-        fa2_bwd_stamp_buf[b][1] = __builtin_amdgcn_s_memrealtime();
-        fa2_bwd_stamp_buf[b][2] = b < ndk ? 0 : 1;
-    }
-#endif
 }
 
 // ---- CuPy face: the reference harness's launch geometry (grid B*H*ceil(S/32),
@@ -2076,16 +1738,16 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     if (nw == 2) return dkdv_launch<D, 2, false>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
     return dkdv_launch<D, 4>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
-template <int D, int NW, int NKB = 2, bool M16 = false, int KS = 1, bool PIPE = false>
+template <int D, int NW, int NKB = 2, bool M16 = false, int KS = 1>
 hipError_t dq_launch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
                      float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
     const long grid = (long)bh * ((S + 32 * (NW / KS) - 1) / (32 * (NW / KS)));
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
     if (o)
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB, M16, KS, PIPE>), dim3((unsigned)grid),
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, true, NKB, M16, KS>), dim3((unsigned)grid),
                            dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     else
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB, M16, KS, PIPE>), dim3((unsigned)grid),
+        hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_f16_kernel<D, NW, false, NKB, M16, KS>), dim3((unsigned)grid),
                            dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     return hipGetLastError();
 }
@@ -2113,7 +1775,7 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
         const bool fits = S % 64 == 0 && S >= 128;
         if (hs == 1 && !fits) return hipErrorInvalidValue;
         const long hgrid = (long)bh * ((S + 255) / 256);
-        if (fits && (hs == 1 || (hs < 0 && nw == 0 && ksp == 0 && !tune_knob("DQ_PIPE", 0) && hgrid >= cu_count()))) {
+        if (fits && (hs == 1 || (hs < 0 && nw == 0 && ksp == 0 && hgrid >= cu_count()))) {
             if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
             hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D>), dim3((unsigned)hgrid), dim3(256), 0, stream, q, k, v,
                                dout, lse, delta, dq, S, o);
@@ -2134,9 +1796,6 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     }
     // 16x16x32 (+2.4 % at C3 over 32x32x16) but at 2 waves
     if constexpr (D <= 64) {
-        // DQ_PIPE: the software-pipelined tile loop (dq_body PIPE)
-        if (nw == 8 && tune_knob("DQ_PIPE", 0))
-            return dq_launch<D, 8, 2, true, 1, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
         if (nw == 8) return dq_launch<D, 8, 2, true>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
         if (nw == 2) return dq_launch<D, 2>(q, k, v, dout, lse, delta, dq, bh, S, o, stream);
     }
@@ -2306,57 +1965,6 @@ hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* 
     return FA2_TILE_LAUNCH(launch_bwd_dkdv)(D, q, k, v, dout, lse, delta, dk, dv, bh, S, stream);
 }
 
-// Single-pass backward (SP).  Which part format a shape gets: 0 = none (the plans
-// above), 1 = fp16 parts, 2 = fp32 parts.  Override BWD_SP (fa2_tune_set); default 0
-// until measured.  Applies to D = 64 on the full grids the two-kernel plan serves.
-int FA2_TILE_LAUNCH(backward_sp_kind)(int D, int bh, int S) {
-    if (D != 64 || bh <= 0 || S <= 0) return 0;
-    if (auto_waves((long)bh * ((S + 31) / 32), 8) < 8) return 0;  // small grids: the fused launch
-    const int k = tune_knob("BWD_SP", 0);
-    return k == 1 || k == 2 ? k : 0;
-}
-size_t FA2_TILE_LAUNCH(backward_workspace_bytes)(int D, int bh, int S) {
-    const int k = FA2_TILE_LAUNCH(backward_sp_kind)(D, bh, S);
-    if (!k) return 0;
-    const size_t nkb = (size_t)(S + 255) / 256;
-    return nkb * (size_t)bh * S * D * (k == 1 ? 2 : 4);
-}
-hipError_t FA2_TILE_LAUNCH(launch_backward_ws)(int D, const float* q, const float* k, const float* v, const float* o,
-                                               const float* dout, const float* lse, float* delta, float* dq,
-                                               float* dk, float* dv, int bh, int S, void* ws, size_t ws_bytes,
-                                               hipStream_t stream) {
-    const int kind = FA2_TILE_LAUNCH(backward_sp_kind)(D, bh, S);
-    if (!kind) return FA2_TILE_LAUNCH(launch_backward)(D, q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, stream);
-    if (!ws || ws_bytes < FA2_TILE_LAUNCH(backward_workspace_bytes)(D, bh, S)) return hipErrorInvalidValue;
-    const long nkb = (S + 255) / 256;
-    const long grid = (long)bh * nkb;
-    const long pstride = (long)bh * S * D;  // elements per key-block slice
-    if (grid > 0x7fffffffL) return hipErrorInvalidValue;
-    if (!FA2_SP_DEL) {
-        const hipError_t e0 = launch_delta(D, dout, o, delta, bh, S, stream);
-        if (e0 != hipSuccess) return e0;
-    }
-    if (kind == 1)
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_sp_f16_kernel<1>), dim3((unsigned)grid), dim3(512), 0, stream, q, k, v,
-                           dout, lse, o, delta, dk, dv, ws, pstride, S);
-    else
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_sp_f16_kernel<2>), dim3((unsigned)grid), dim3(512), 0, stream, q, k, v,
-                           dout, lse, o, delta, dk, dv, ws, pstride, S);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (tune_knob("BWD_SP_NORED", 0)) return hipSuccess;  // diagnostics: the first launch alone
-    const long n8 = pstride / 8;
-    long rg = (n8 + 255) / 256;
-    if (rg > 8192) rg = 8192;
-    if (kind == 1)
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_sp_reduce<1>), dim3((unsigned)rg), dim3(256), 0, stream, ws, pstride,
-                           (int)nkb, dq, n8);
-    else
-        hipLaunchKernelGGL((fa2f16b::fa2_bwd_sp_reduce<2>), dim3((unsigned)rg), dim3(256), 0, stream, ws, pstride,
-                           (int)nkb, dq, n8);
-    return hipGetLastError();
-}
-
 }  // namespace fa2
 
 // Host API with the reference's semantics (f-attn2-backward_f16.cu:375-474).
@@ -2420,15 +2028,3 @@ extern "C" __global__ void D_computation_reduction_kernel_wrapper(const float* d
     fa2f16b::delta_row_body(d_output, output, (long)batch_size * num_heads * seq_len, head_dim, d);
 }
 #endif  // CUPY_INLINE_COMPILE
-
-#if defined(FA2_STAMPS) && !defined(FA2_TILE_BF16) && !defined(CUPY_INLINE_COMPILE)
-// timing-only builds (tools/stamps_small.py): copy the fused backward's per-workgroup
-// stamps [slot][entry, done, role, -] to host memory
-extern "C" int fa2_bwd_stamps_read(void* host, size_t bytes) {
-    if (bytes > sizeof(fa2f16b::fa2_bwd_stamp_buf)) bytes = sizeof(fa2f16b::fa2_bwd_stamp_buf);
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(fa2f16b::fa2_bwd_stamp_buf), bytes, 0, hipMemcpyDeviceToHost) ==
-                   hipSuccess
-               ? 0
-               : -1;
-}
-#endif

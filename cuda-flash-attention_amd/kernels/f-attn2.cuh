@@ -120,22 +120,6 @@ hipError_t launch_bwd_dq_delta_bf16(int D, const float* q, const float* k, const
                                     const float* dout, const float* lse, float* delta, float* dq, int bh, int S,
                                     hipStream_t stream);
 
-// Single-pass backward with a caller workspace (fa2_backward_ws): dK, dV, Δ and per-key-
-// block dQ parts in one launch, then an ordered sum of the parts.  backward_workspace_bytes
-// is 0 where the shape takes the plans of launch_backward_* (then launch_backward_ws runs
-// those and ignores the workspace).
-size_t backward_workspace_bytes_f16(int D, int bh, int S);
-size_t backward_workspace_bytes_bf16(int D, int bh, int S);
-hipError_t launch_backward_ws_f16(int D, const float* q, const float* k, const float* v, const float* o,
-                                  const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
-                                  int bh, int S, void* ws, size_t ws_bytes, hipStream_t stream);
-hipError_t launch_backward_ws_bf16(int D, const float* q, const float* k, const float* v, const float* o,
-                                   const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
-                                   int bh, int S, void* ws, size_t ws_bytes, hipStream_t stream);
-
-// compute units of the current device (cached)
-int cu_count();
-
 inline bool supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
 // Launch-plan override `name` as set by fa2_tune_set (include/fa2_amd.h), else `dflt`

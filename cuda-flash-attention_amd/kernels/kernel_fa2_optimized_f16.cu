@@ -533,16 +533,6 @@ __device__ __forceinline__ void fwd_store(const FwdState<D>& st, float* O, float
 //
 // NKB 32-key blocks per KV tile (2: 64-key tiles; 1: 32-key tiles, fewer registers
 // for D = 128 at 8 waves).
-//
-// FA2_STAMPS (timing-only builds, tools/stamps_small.py): thread 0 of each workgroup
-// records s_memrealtime (100 MHz) at phase boundaries and writes the stamps over the
-// first 16 floats of its block's first O row at the end (results are then invalid)
-#ifdef FA2_STAMPS
-#define FA2_STAMP(i) \
-    if (tid == 0) stamp[i] = __builtin_amdgcn_s_memrealtime()
-#else
-#define FA2_STAMP(i)
-#endif
 
 // KS > 1 (small grids): the key range is split over KS wave groups of NQ = NW / KS
 // waves.  Wave w handles query rows of slot w % NQ against tiles j·KS + w / NQ;
@@ -574,10 +564,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
     __shared__ __attribute__((aligned(16))) float ostage[NQ][32][36];  // per-wave O block stage
 
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
-#ifdef FA2_STAMPS
-    unsigned long long stamp[8] = {};
-#endif
-    FA2_STAMP(0);
     const int wave = KS > 1 ? (tid >> 6) % NQ : tid >> 6;  // query slot of the wave
     const int kg = KS > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) / NQ) : 0;  // key group
     const int nqb = (S + QW * NQ - 1) / (QW * NQ);
@@ -617,7 +603,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             vs.store(smem + KS * TILE, 1.f, tid);
         }
         __syncthreads();
-        FA2_STAMP(1);
         fwd_init<D, SEED>(st[0], nullptr, 0, S, S, h);  // state only (q >= S: no Q read)
 #pragma unroll
         for (int t = 0; t < D / 16; ++t) st[0].qf[t] = fo.rowop(qblk, wave * QW, t);
@@ -705,9 +690,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             __syncthreads();
             return b;
         };
-        FA2_STAMP(2);
         step(smem, smem + KS * TILE, smem + 2 * KS * TILE, smem + 3 * KS * TILE, 0, 1 < nsteps);
-        FA2_STAMP(3);
         // D <= 64: the ragged last tile's step (always the last one) runs after the loop
         // (r03 A/B: B2_H8 fwd S = 512 -7 %, S = 1024 -5 %, C3 -1.2 %); D = 128 keeps it
         // in the loop (peeled, its 32-key-tile loop ran 5.8 % slower at C4)
@@ -729,7 +712,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
             _Float16* const kc = (jend & 1) ? smem + 2 * KS * TILE : smem;
             bad = stepf(MaskTag<1>{}, kc, kc + KS * TILE, smem, smem, jend, false) || bad;
         }
-        FA2_STAMP(4);
         if (__syncthreads_or(bad)) {
             // every wave restages; only the waves that saw a spike reset and recompute (the
             // others' O, l and m never left range and stand as they are)
@@ -787,7 +769,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         st[0].l[0] = l;
         st[0].l[1] = st[0].l[2] = st[0].l[3] = 0.f;
     }
-    FA2_STAMP(5);
     // O through a wave-private LDS stage, one 32x32 block at a time, stored as whole
     // 128-B row segments (8 rows per instruction) instead of 16-B pieces of 32 rows
     {
@@ -810,16 +791,6 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
         }
         if (h == 0 && q0 < S) LSE[(long)bh * S + q0] = st[0].m * FA2_LN2 + __logf(lt);
     }
-#ifdef FA2_STAMPS
-    FA2_STAMP(6);
-    __builtin_amdgcn_s_waitcnt(0);  // every store of this wave complete
-    FA2_STAMP(7);
-    if (tid == 0) {
-        unsigned long long* dst = reinterpret_cast<unsigned long long*>(O + base + (long)qb * QW * NQ * D);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dst[i] = stamp[i];
-    }
-#endif
 }
 
 #ifndef CUPY_INLINE_COMPILE
@@ -1041,9 +1012,12 @@ namespace fa2 {
 
 // KS > 1: NW / KS query waves per workgroup (D = 64: 32-key tiles -- with 64-key
 // tiles the KS-tile staging registers spill)
+// nkb_req: a FWD_NKB override (0 = none); an instance of other tiles is an error, never
+// a silent launch of the plan the override asked to leave
 template <int D, int NW, int KS = 1, int NKB = (KS == 1 || D <= 32 ? 2 : 1)>
 static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
-                                 hipStream_t stream) {
+                                 hipStream_t stream, int nkb_req) {
+    if (nkb_req && nkb_req != NKB) return hipErrorInvalidValue;
     const int nqb = (S + 32 * (NW / KS) - 1) / (32 * (NW / KS));
     const long grid = (long)bh * nqb;
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
@@ -1123,21 +1097,21 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
         // MFMAs per barrier of the 32-key tiles): B2_H8_S2048 fwd 29.6 -> 25.4 us, step
         // 99.1 -> 95.7; B4_H8_S1024 fwd 18.1 -> 15.8; S = 1500 22.3 -> 19.1
         // (profiles/r04/nkb/).  KS = 4 keeps 32-key tiles at 8 waves (64-key tiles spill).
-        if (ks == 2 && nw == 8 && nkb != 1) return fwd_f16_launch<D, 8, 2, 2>(q, k, v, o, lse, bh, S, stream);
-        if (ks == 2 && nw == 8) return fwd_f16_launch<D, 8, 2, 1>(q, k, v, o, lse, bh, S, stream);
-        if (ks == 4 && nw == 4 && nkb == 2) return fwd_f16_launch<D, 4, 4, 2>(q, k, v, o, lse, bh, S, stream);
-        if (ks == 4 && nw == 8) return fwd_f16_launch<D, 8, 4>(q, k, v, o, lse, bh, S, stream);
-        if (ks == 4 && nw == 4) return fwd_f16_launch<D, 4, 4>(q, k, v, o, lse, bh, S, stream);
-        if (ks == 2 && nw == 4) return fwd_f16_launch<D, 4, 2>(q, k, v, o, lse, bh, S, stream);
+        if (ks == 2 && nw == 8 && nkb != 1) return fwd_f16_launch<D, 8, 2, 2>(q, k, v, o, lse, bh, S, stream, 0);
+        if (ks == 2 && nw == 8) return fwd_f16_launch<D, 8, 2, 1>(q, k, v, o, lse, bh, S, stream, 0);
+        if (ks == 4 && nw == 4 && nkb == 2) return fwd_f16_launch<D, 4, 4, 2>(q, k, v, o, lse, bh, S, stream, 0);
+        if (ks == 4 && nw == 8) return fwd_f16_launch<D, 8, 4>(q, k, v, o, lse, bh, S, stream, nkb);
+        if (ks == 4 && nw == 4) return fwd_f16_launch<D, 4, 4>(q, k, v, o, lse, bh, S, stream, nkb);
+        if (ks == 2 && nw == 4) return fwd_f16_launch<D, 4, 2>(q, k, v, o, lse, bh, S, stream, nkb);
     }
     if constexpr (D <= 64) {
-        if (nw == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream);
+        if (nw == 8) return fwd_f16_launch<D, 8>(q, k, v, o, lse, bh, S, stream, nkb);
     } else {
         // D = 128 at 8 waves only with 32-key tiles (64-key tiles spill)
-        if (nw == 8) return fwd_f16_launch<D, 8, 1, 1>(q, k, v, o, lse, bh, S, stream);
+        if (nw == 8) return fwd_f16_launch<D, 8, 1, 1>(q, k, v, o, lse, bh, S, stream, nkb);
     }
-    if (nw == 2) return fwd_f16_launch<D, 2>(q, k, v, o, lse, bh, S, stream);
-    return fwd_f16_launch<D, 4>(q, k, v, o, lse, bh, S, stream);
+    if (nw == 2) return fwd_f16_launch<D, 2>(q, k, v, o, lse, bh, S, stream, nkb);
+    return fwd_f16_launch<D, 4>(q, k, v, o, lse, bh, S, stream, nkb);
 }
 
 hipError_t FA2_TILE_LAUNCH(launch_forward)(int D, const float* q, const float* k, const float* v, float* o, float* lse, int bh,

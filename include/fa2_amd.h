@@ -65,17 +65,6 @@ int fa2_backward(const float* q, const float* k, const float* v, const float* o,
                  const float* lse, float* delta, float* dq, float* dk, float* dv, int batch, int heads, int seq,
                  int head_dim, int precision, void* stream);
 
-/* Backward with a caller-provided device workspace.  Where the shape allows it (D = 64 on
- * full grids, FA2_FP16 / FA2_BF16) this may run the single-pass plan: dK, dV, Δ and one dQ
- * part per 256-key block in one launch, then an ordered sum of the parts (bitwise
- * reproducible).  fa2_backward_workspace_size gives the bytes that plan needs, 0 where
- * fa2_backward's plans run (fa2_backward_ws then ignores the workspace).  Same outputs
- * and contract as fa2_backward otherwise. */
-int fa2_backward_workspace_size(int batch, int heads, int seq, int head_dim, int precision, size_t* bytes);
-int fa2_backward_ws(const float* q, const float* k, const float* v, const float* o, const float* dout,
-                    const float* lse, float* delta, float* dq, float* dk, float* dv, int batch, int heads, int seq,
-                    int head_dim, int precision, void* workspace, size_t workspace_bytes, void* stream);
-
 /* The two MFMA kernels of the fp16 backward, separately (profiling/bench hooks;
  * fa2_delta + these two compute what fa2_backward with FA2_FP16 does). */
 int fa2_backward_dkdv(const float* q, const float* k, const float* v, const float* dout, const float* lse,
@@ -137,9 +126,10 @@ int fa2_shard_range(int total_heads, int shards, int index, int* first, int* cou
 /* Launch-plan override (tests and tuning tools only; nothing is read from the
  * environment).  fa2_tune_set("DKDV_QS", 2) makes the next launches use that plan
  * where the shape allows it; fa2_tune_set(NULL, 0) clears every override.  Knobs:
- * FWD_WAVES, FWD_KS, FWD_NKB, DKDV_WAVES, DKDV_QS, DQ_WAVES, DQ_KS, BWD_FUSED,
- * BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW, DQ_PIPE, BWD_SP (see the launchers in
- * kernels/), and
+ * FWD_HS, FWD_WAVES, FWD_KS, FWD_NKB, DKDV_HS, DKDV_WAVES, DKDV_QS, DQ_HS, DQ_WAVES,
+ * DQ_KS, BWD_FUSED, BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW (see the launchers in
+ * kernels/; a value that forces a plan the shape cannot take is FA2_E_INVALID at the
+ * launch, never a silent fallback), and
  * the test-only HOST_SHARDS_ON_DEVICE0 = 1 (fa2_*_host run every shard on device 0,
  * so an N-way split's head offsets are testable on one GPU) and HOST_CHUNKS (head
  * chunks of the fa2_*_host pipeline; 0 = auto).  Any other name:

@@ -3,7 +3,7 @@
 loop (is a kernel at the power cap?  then its time follows its energy, not its stalls).
 
   python tools/power_probe.py --shape 4,16,2048,64 --kernel fwd --kernel dqd --kernel dkdv --seconds 4
-  python tools/power_probe.py --kernel dqd --variant DQ_PIPE=0,DQ_WAVES=8 --variant DQ_PIPE=1,DQ_WAVES=8
+  python tools/power_probe.py --kernel dqd --variant DQ_HS=0 --variant DQ_HS=1
 
 A background thread samples `amd-smi metric -p -c` every ~0.2 s while the kernel loop
 runs; the first 0.6 s of each loop (clock ramp) are discarded.  Energy per call =
