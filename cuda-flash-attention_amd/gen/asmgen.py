@@ -255,6 +255,20 @@ def ablate(seq):
     return out
 
 
+def stamp(sv):
+    """'stamps' timing builds: s_memtime into lane s98 of v{sv} (s98 counts the stamps; the
+    drain keeps the counted waits exact around the scalar-memory return); not a product path"""
+    if "stamps" not in ABL:
+        return []
+    return [Ins("s_memtime s[96:97]", "salu", [], ["s96", "s97"]), Ins("s_waitcnt lgkmcnt(0)", "wait"),
+            Ins("s_mov_b32 m0, s98", "salu", R(["s98"]), ["m0"]), Ins("s_nop 4", "nop"),
+            Ins(f"v_writelane_b32 v{sv}, s96, m0", "valu", R(["s96", "m0"]), [f"v{sv}"]),
+            Ins("s_add_u32 s98, s98, 1", "salu", R(["s98"]), ["s98", "scc"])]
+
+
+STAMP_CLOBBERS = ['"s96"', '"s97"', '"s98"', '"m0"']
+
+
 def parse_abl(argv):
     if "--abl" in argv:
         ABL.update(argv[argv.index("--abl") + 1].split(","))

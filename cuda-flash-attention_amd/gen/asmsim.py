@@ -463,6 +463,8 @@ class Wave:
                 self.lgkm.append(([], lambda: None))
             elif op.startswith("v_mfma_f32_32x32x16"):
                 self.mfma(args)
+            elif op.startswith("v_mfma_f32_16x16x32"):
+                self.mfma16(args)
             elif op == "v_exp_f32":
                 (f, k), = self.regs(args[0])
                 x = u2f(self.vsrc(args[1]))
@@ -550,6 +552,34 @@ class Wave:
             for i in range(16):
                 m = (i & 3) + 8 * (i >> 2) + 4 * (l // 32)
                 out[i, l] = np.float32(C[i, l] + P[m, l % 32])
+        for i, (f, k) in enumerate(dst):
+            self.put(f, k, f2u(out[i]))
+
+
+    def mfma16(self, args):
+        """v_mfma_f32_16x16x32: A[l % 16][8 (l / 16) + j], B[8 (l / 16) + j][l % 16],
+        D reg i -> row 4 (l / 16) + i, column l % 16"""
+        sim = self.sim
+        dst = self.regs(args[0])
+        A = np.stack([self.get(f, k) for f, k in self.regs(args[1])])
+        B = np.stack([self.get(f, k) for f, k in self.regs(args[2])])
+        C = np.zeros((4, 64), np.float32) if args[3] == "0" else np.stack(
+            [u2f(self.get(f, k)) for f, k in self.regs(args[3])])
+
+        def halves(X):
+            return np.stack([sim.from16(X[e // 2] >> (16 * (e % 2))) for e in range(8)], axis=1)
+        a, b = halves(A).astype(np.float64), halves(B).astype(np.float64)
+        Am = np.zeros((16, 32))
+        Bm = np.zeros((32, 16))
+        for l in range(64):
+            for j in range(8):
+                Am[l % 16, 8 * (l // 16) + j] = a[l, j]
+                Bm[8 * (l // 16) + j, l % 16] = b[l, j]
+        P = Am @ Bm
+        out = np.zeros((4, 64), np.float32)
+        for l in range(64):
+            for i in range(4):
+                out[i, l] = np.float32(C[i, l] + P[4 * (l // 16) + i, l % 16])
         for i, (f, k) in enumerate(dst):
             self.put(f, k, f2u(out[i]))
 

@@ -39,7 +39,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import asmgen  # noqa: E402
-from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402
+from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, stamp, tagged, valu  # noqa: E402,E501
 
 KT = 64
 ROWS = 256
@@ -62,6 +62,9 @@ class Cfg:
         self.mf = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvt = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
         self.nvgpr, self.nagpr = 224, 224
+        self.SV = self.nvgpr  # 'stamps' timing builds: the stamp register (and one more)
+        if "stamps" in asmgen.ABL:
+            self.nvgpr += 2
 
     # AGPRs
     def O(self, c, b):
@@ -229,15 +232,20 @@ def body(cfg, p, log):
     conv = staging_convert(cfg, 0, q)
     for ins in conv:
         ins.earliest = 4
+    seq += stamp(cfg.SV)
     seq += schedule_phase(cfg, sdp_mfmas(cfg, 0), [ds_part(cfg, 1, PART2), conv], f"P1.{p}", log)
+    seq += stamp(cfg.SV)
     seq += schedule_phase(cfg, dq_mfmas(cfg, 1), [ds_part(cfg, 0, PART1), staging_convert(cfg, 1, q),
                                                   staging_loads(cfg, 0)], f"P2.{p}", log)
+    seq += stamp(cfg.SV)
     kt = []
     for i in range(cfg.NF):
         kt += ktr_reads(cfg, i, p)
     seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [ds_part(cfg, 0, PART2), kt], f"P3.{p}", log)
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
+    seq += stamp(cfg.SV)
     seq.append(tagged("bar", [Ins("s_barrier", "bar")])[0])
+    seq += stamp(cfg.SV)
     seq += schedule_phase(cfg, dq_mfmas(cfg, 0), [ds_part(cfg, 1, PART1), row_reads(cfg, q, 0) + row_reads(cfg, q, 1),
                                                   staging_loads(cfg, 1) + [goff_inc(cfg)]], f"P4.{p}", log)
     return seq
@@ -245,7 +253,9 @@ def body(cfg, p, log):
 
 def prologue(cfg):
     D, NTQ = cfg.D, cfg.NTQ
-    seq = staging_loads(cfg, 0) + staging_loads(cfg, 1) + [goff_inc(cfg)]
+    seq = [Ins("s_mov_b32 s98, 0", "salu", [], ["s98"])] if "stamps" in asmgen.ABL else []
+    seq += stamp(cfg.SV)
+    seq += staging_loads(cfg, 0) + staging_loads(cfg, 1) + [goff_inc(cfg)]
     # Q and dO fragments of both chains (blocks in LDS at %[qb] / %[db] + this wave's rows)
     for t in range(NTQ):
         seq.append(valu(f"v_add_u32 v{t}, %[qb], %[ka{t}]", [], [f"v{t}"]))
@@ -275,11 +285,13 @@ def prologue(cfg):
     seq += staging_loads(cfg, 0) + staging_loads(cfg, 1) + [goff_inc(cfg)]
     seq += [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_barrier", "bar")]
     seq += row_reads(cfg, 1, 0) + row_reads(cfg, 1, 1)
+    seq += stamp(cfg.SV)
     return seq
 
 
 def epilogue(cfg):
     seq = [Ins("s_waitcnt vmcnt(0) lgkmcnt(0)", "wait")]
+    seq += stamp(cfg.SV)
     seq += ds_part(cfg, 1, PART2)
     seq += dq_mfmas(cfg, 1)
     seq.append(Ins("s_barrier", "bar"))
@@ -289,6 +301,18 @@ def epilogue(cfg):
                 r = cfg.O(c, b) + 4 * g
                 off = (c * 32 * cfg.OST + 32 * b + 8 * g) * 4
                 seq.append(Ins(f"ds_write_b128 %[oa], {rtxt('a', r, 4)} offset:{off}", "dsw", R(rng("a", r, 4)), []))
+    if "stamps" in asmgen.ABL:
+        # the stamps into stage columns 2 / 6, the count into 3 / 7 (gen_fwd_hs.py's layout)
+        seq += stamp(cfg.SV)
+        sv, sc = cfg.SV, cfg.SV + 1
+        seq += [Ins("s_nop 4", "nop"),
+                valu(f"v_and_b32 v{sv}, 0xffffff, v{sv}", [f"v{sv}"], [f"v{sv}"]),
+                valu(f"v_cvt_f32_u32 v{sv}, v{sv}", [f"v{sv}"], [f"v{sv}"]),
+                valu(f"v_mov_b32 v{sc}, s98", [], [f"v{sc}"]),
+                valu(f"v_cvt_f32_u32 v{sc}, v{sc}", [f"v{sc}"], [f"v{sc}"]),
+                Ins("s_nop 4", "nop"),
+                Ins(f"ds_write_b32 %[oa], v{sv} offset:8", "dsw", R([f"v{sv}"]), []),
+                Ins(f"ds_write_b32 %[oa], v{sc} offset:12", "dsw", R([f"v{sc}"]), [])]
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     return seq
 
@@ -333,6 +357,8 @@ def operands(cfg):
     ins += ['[lo] "v"(hs_lo)', '[oa] "v"(hs_oa)', '[nl0] "v"(hs_nl0)', '[nl1] "v"(hs_nl1)', '[nd0] "v"(hs_nd0)',
             '[nd1] "v"(hs_nd1)', '[rsk] "s"(hs_rsk)', '[rsv] "s"(hs_rsv)', '[qb] "s"(hs_qb)', '[db] "s"(hs_db)']
     clob = [f'"v{i}"' for i in range(cfg.nvgpr)] + [f'"a{i}"' for i in range(cfg.nagpr)] + ['"vcc"', '"scc"', '"memory"']
+    if "stamps" in asmgen.ABL:
+        clob += asmgen.STAMP_CLOBBERS
     return outs, ins, clob
 
 

@@ -48,7 +48,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import asmgen  # noqa: E402
-from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402,E501
+from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, stamp, tagged, valu  # noqa: E402,E501
 
 KT = 64  # keys per tile
 NWAVE = 4
@@ -73,6 +73,9 @@ class Cfg:
         self.STG = 128
         self.MB = self.STG + 16 * self.CPT
         self.nvgpr = self.MB + 16
+        self.SV = self.nvgpr  # 'stamps' timing builds: the stamp register (and one more)
+        if "stamps" in asmgen.ABL:
+            self.nvgpr += 2
         self.TBB = KT * D * 2  # bytes of one fp16 tile image
         self.OST = D + 4  # O stage row stride (floats)
         self.mf = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
@@ -281,7 +284,9 @@ def body(cfg, p, log):
     conv = staging_convert(cfg, 0, q)
     for ins in conv:
         ins.earliest = len(qk_mfmas(cfg, 0, ring)) // 4
+    seq += stamp(cfg.SV)
     seq += schedule_phase(cfg, qk_mfmas(cfg, 0, ring), [softmax_part(cfg, 1, 1, True), kreads, conv], f"P1.{p}", log)
+    seq += stamp(cfg.SV)
     # P2: PV of chain B (tile j-1) | softmax A (j) first half, V(j+1) staged, K(j+2) loads,
     #     K re-read 0..7 (D=128), first V(j) fragments into freed Vf slots
     nsplit = cfg.NF // 4 if cfg.D > 64 else 0
@@ -302,9 +307,12 @@ def body(cfg, p, log):
     vre = []
     for i in range(nsplit, cfg.NF):
         vre += vfrag_reads(cfg, i, p)
+    seq += stamp(cfg.SV)
     seq += schedule_phase(cfg, qk_mfmas(cfg, 1, ring), [softmax_part(cfg, 0, 1, True), kreads, vre], f"P3.{p}", log)
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
+    seq += stamp(cfg.SV)
     seq.append(Ins("s_barrier", "bar"))
+    seq += stamp(cfg.SV)
     # P4: PV of chain A (tile j) | softmax B (j) first half, K(j+1) fragment prefetch, V(j+2) loads
     pre = [kfrag_read(cfg, f, q, cfg.Kr(f)) for f in range(min(cfg.ring, NKF))]
     seq += schedule_phase(cfg, pv_mfmas(cfg, 0), [softmax_part(cfg, 1, 0, False), pre,
@@ -314,7 +322,9 @@ def body(cfg, p, log):
 
 def prologue(cfg):
     D, NTQ, NKF = cfg.D, cfg.NTQ, cfg.NKF
-    seq = [Ins("s_mov_b64 %[flg], 0", "salu", [], ["s:flg"]),
+    seq = [Ins("s_mov_b32 s98, 0", "salu", [], ["s98"])] if "stamps" in asmgen.ABL else []
+    seq += stamp(cfg.SV)
+    seq += [Ins("s_mov_b64 %[flg], 0", "salu", [], ["s:flg"]),
            valu(f"v_mov_b32 v{cfg.l(0)}, 0", [], [f"v{cfg.l(0)}"]),
            valu(f"v_mov_b32 v{cfg.l(1)}, 0", [], [f"v{cfg.l(1)}"])]
     # tile 1 loads (K then V)
@@ -374,12 +384,14 @@ def prologue(cfg):
     seq += staging_loads(cfg, 0) + staging_loads(cfg, 1) + [goff_inc(cfg)]
     seq += [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_barrier", "bar")]
     seq += [kfrag_read(cfg, f, 1, cfg.Kr(f)) for f in range(min(cfg.ring, NKF))]
+    seq += stamp(cfg.SV)
     return seq
 
 
 def epilogue(cfg):
     D = cfg.D
     seq = [Ins("s_waitcnt vmcnt(0) lgkmcnt(0)", "wait")]
+    seq += stamp(cfg.SV)
     seq += softmax_part(cfg, 1, 1, True)
     seq += pv_mfmas(cfg, 1)
     # every wave is done with the tile slots before the O stage overwrites them
@@ -393,6 +405,20 @@ def epilogue(cfg):
     for c in range(2):
         seq.append(valu(f"v_mov_b32 %[om{c}], v{cfg.m(c)}", [f"v{cfg.m(c)}"], []))
         seq.append(valu(f"v_mov_b32 %[ol{c}], v{cfg.l(c)}", [f"v{cfg.l(c)}"], []))
+    if "stamps" in asmgen.ABL:
+        # the stamps into O columns 2 / 6 of the wave's rows r (lanes r / 32 + r) and the stamp
+        # count into columns 3 / 7; l = 1/2 per lane half, so the epilogue stores the stage as is
+        seq += stamp(cfg.SV)
+        sv, sc = cfg.SV, cfg.SV + 1
+        seq += [Ins("s_nop 4", "nop"),
+                valu(f"v_and_b32 v{sv}, 0xffffff, v{sv}", [f"v{sv}"], [f"v{sv}"]),
+                valu(f"v_cvt_f32_u32 v{sv}, v{sv}", [f"v{sv}"], [f"v{sv}"]),
+                valu(f"v_mov_b32 v{sc}, s98", [], [f"v{sc}"]),
+                valu(f"v_cvt_f32_u32 v{sc}, v{sc}", [f"v{sc}"], [f"v{sc}"]),
+                Ins("s_nop 4", "nop"),
+                Ins(f"ds_write_b32 %[oa], v{sv} offset:8", "dsw", R([f"v{sv}"]), []),
+                Ins(f"ds_write_b32 %[oa], v{sc} offset:12", "dsw", R([f"v{sc}"]), []),
+                valu("v_mov_b32 %[ol0], 0.5", [], []), valu("v_mov_b32 %[ol1], 0.5", [], [])]
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     return seq
 
@@ -445,6 +471,8 @@ def operands(cfg):
     ins += [f'[vo{c}] "v"(hs_vo[{c}])' for c in range(cfg.CPT)]
     ins += ['[lo] "v"(hs_lo)', '[oa] "v"(hs_oa)', '[rsk] "s"(hs_rsk)', '[rsv] "s"(hs_rsv)', '[qb] "s"(hs_qb)']
     clob = [f'"v{i}"' for i in range(cfg.nvgpr)] + [f'"a{i}"' for i in range(cfg.nagpr)] + ['"vcc"', '"scc"', '"memory"']
+    if "stamps" in asmgen.ABL:
+        clob += asmgen.STAMP_CLOBBERS
     return outs, ins, clob
 
 
