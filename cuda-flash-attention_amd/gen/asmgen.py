@@ -71,7 +71,7 @@ def schedule_phase(cfg, mfmas, streams, name, log):
     tot = [max(1, sum(i.cost for i in s)) for s in streams]
     done = [0] * len(streams)
     total = sum(sum(i.cost for i in s) for s in streams)
-    cap = max(24, -(-total // max(1, nM)))
+    cap = max(getattr(cfg, "min_cap", 24), -(-total // max(1, nM)))
     out = []
     for g in range(nM + 1):
         used = 0

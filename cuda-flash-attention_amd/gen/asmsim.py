@@ -181,12 +181,14 @@ class Sim:
                     LSE[R] = m[q] * np.log(2.0) + np.log(lt[q])
         return O, LSE, flag, waves
 
-    def run_dq(self, dO, LSE, Delta):
-        """fa2_bwd_dq_hs_kernel<64>: the C++ prologue, the asm of fa2_bwd_dq_hs.inc, the dQ rows"""
+    def run_dq(self, dO, LSE, Delta, m16=False):
+        """fa2_bwd_dq_hs_kernel<64, m16>: the C++ prologue, the asm of fa2_bwd_dq_hs.inc
+        (m16: fa2_bwd_dq16_hs.inc), the dQ rows"""
         import gen_bwd_dq as GD
+        import gen_bwd_dq16 as GD16
         SWZ[0] = swz_bwd
         D = self.D
-        cfg = GD.Cfg(D, self.bf16)
+        cfg = (GD16 if m16 else GD).Cfg(D, self.bf16)
         TB = 64 * D
         self.lds = np.zeros(cfg.lds_bytes // 4, np.uint32)
         q0 = self.block * 256
@@ -202,7 +204,12 @@ class Sim:
         ct = 16 * (g & 1) + 4 * (i16 & 3)
         kt = [[np.array([2 * tile_off(D, int(rt[l]) + 8 * k, 32 * b + int(ct[l])) for l in lanes]) for k in range(2)]
               for b in range(D // 32)]
-        text = self.asm_text("fa2_bwd_dq_hs.inc", "FA2_DQ_ASM")
+        if m16:
+            ka = [np.array([2 * tile_off(D, int(i16[l]), 32 * ks + 8 * int(g[l])) for l in lanes]) for ks in range(D // 32)]
+            kt = [[np.array([2 * tile_off(D, 16 * k + 4 * int(g[l]) + (int(i16[l]) >> 2), 16 * db + 4 * (int(i16[l]) & 3))
+                             for l in lanes]) for k in range(2)] for db in range(D // 16)]
+        text = self.asm_text("fa2_bwd_dq16_hs.inc", "FA2_DQ16_ASM") if m16 else \
+            self.asm_text("fa2_bwd_dq_hs.inc", "FA2_DQ_ASM")
         waves = []
         for w in range(4):
             tid = 64 * w + lanes
@@ -216,15 +223,18 @@ class Sim:
                     lo = 2 * np.array([row[l] * D + ((ch[l] ^ SWZ[0](D, int(row[l]))) << 3) for l in lanes])
             ops = {"qb": 4 * TB * 2 + w * 64 * D * 2, "db": 8 * TB * 2 + w * 64 * D * 2, "cnt": self.S // 64 - 1,
                    "goff": 64 * D * 4, "oa": ((w * 64 + r) * cfg.OST + 4 * h) * 4, "lo": lo, "rsk": "K", "rsv": "V"}
-            for c in range(2):
-                qq = q0 + w * 64 + c * 32 + r
+            nblk, rows = (4, lambda c: 16 * c + i16) if m16 else (2, lambda c: 32 * c + r)
+            for c in range(nblk):
+                qq = q0 + w * 64 + rows(c)
                 ok = qq < self.S
                 nl = np.where(ok, -LSE[np.minimum(qq, self.S - 1)] * LOG2E, -np.inf).astype(np.float32)
                 nd = np.where(ok, -Delta[np.minimum(qq, self.S - 1)], 0).astype(np.float32)
                 ops[f"nl{c}"], ops[f"nd{c}"] = f2u(nl), f2u(nd)
-            for t in range(D // 16):
+            if m16:
+                ops["oa"] = ((w * 64 + i16) * cfg.OST + 4 * g) * 4
+            for t in range(len(ka)):
                 ops[f"ka{t}"] = ka[t]
-            for b in range(D // 32):
+            for b in range(len(kt)):
                 for k in range(2):
                     ops[f"kt{b}_{k}"] = kt[b][k]
             for c in range(D // 32):
@@ -591,7 +601,7 @@ def main():
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--spike", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", choices=["fwd", "dq", "dkdv"], default="fwd")
+    ap.add_argument("--kernel", choices=["fwd", "dq", "dq16", "dkdv"], default="fwd")
     a = ap.parse_args()
     rng = np.random.RandomState(0)
     S, D = a.S, a.D
@@ -617,7 +627,7 @@ def main():
         tol = 2e-2 if a.bf16 else 1e-2
         assert ek < tol and ev < tol, "mismatch"
         return
-    if a.kernel == "dq":
+    if a.kernel in ("dq", "dq16"):
         dO = rng.randn(S, D).astype(np.float32)
         s64 = (Q.astype(np.float64) @ K.T.astype(np.float64)) / np.sqrt(D)
         mx = s64.max(1, keepdims=True)
@@ -628,7 +638,7 @@ def main():
         dS = P * (dO.astype(np.float64) @ V.T.astype(np.float64) - delta[:, None])
         edq = dS @ K.astype(np.float64) / np.sqrt(D)
         sim = Sim(D, a.bf16, S, Q, K, V, a.block)
-        dq = sim.run_dq(dO, lse.astype(np.float32), delta.astype(np.float32))
+        dq = sim.run_dq(dO, lse.astype(np.float32), delta.astype(np.float32), m16=a.kernel == "dq16")
         q0 = a.block * 256
         nq = min(256, S - q0)
         err = np.abs(dq[:nq] - edq[q0:q0 + nq]).max()

@@ -1209,9 +1209,15 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
 #define FA2_DQ_INC "fa2_bwd_dq_hs.inc"  // (timing-only ablation builds name another, tools/r05_hs_abl.sh)
 #endif
 #include FA2_DQ_INC
+#ifndef FA2_DQ16_INC
+#define FA2_DQ16_INC "fa2_bwd_dq16_hs.inc"
+#endif
+#include FA2_DQ16_INC
 namespace fa2f16b {
 
-template <int D>
+// M16: the loop on v_mfma_f32_16x16x32 (fa2_bwd_dq16_hs.inc, gen/gen_bwd_dq16.py): 16-row
+// query blocks on the lane, seeds per 16-row block, dQᵀ tiles of 16 d x 16 queries
+template <int D, bool M16>
 __global__ void __launch_bounds__(256, 1)
 fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                      const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
@@ -1263,32 +1269,68 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
     vs.store(smem + 2 * TB, 1.f, tid);
     __syncthreads();
 
-    FragOffsets<D> fo;
-    fo.init(lane);
-    int hs_ka[D / 16], hs_kt[D / 32][2], hs_vo[D / 32];
+    // per-lane LDS byte offsets of the row and transposed fragment reads (the 32x32x16 or
+    // the 16x16x32 operand maps)
+    constexpr int NKA = M16 ? D / 32 : D / 16, NKT = M16 ? D / 16 : D / 32;
+    int hs_ka[NKA], hs_kt[NKT][2], hs_vo[D / 32];
+    if constexpr (M16) {
+        FragOffsets16<D> fo;
+        fo.init(lane);
 #pragma unroll
-    for (int t = 0; t < D / 16; ++t) hs_ka[t] = fo.row[t] * 2;
+        for (int t = 0; t < NKA; ++t) hs_ka[t] = fo.row[t] * 2;
 #pragma unroll
-    for (int b = 0; b < D / 32; ++b) {
-        hs_kt[b][0] = fo.tr[b][0] * 2;
-        hs_kt[b][1] = fo.tr[b][1] * 2;
+        for (int b = 0; b < NKT; ++b) {
+            hs_kt[b][0] = fo.tr[b][0] * 2;
+            hs_kt[b][1] = fo.tr[b][1] * 2;
+        }
+    } else {
+        FragOffsets<D> fo;
+        fo.init(lane);
+#pragma unroll
+        for (int t = 0; t < NKA; ++t) hs_ka[t] = fo.row[t] * 2;
+#pragma unroll
+        for (int b = 0; b < NKT; ++b) {
+            hs_kt[b][0] = fo.tr[b][0] * 2;
+            hs_kt[b][1] = fo.tr[b][1] * 2;
+        }
     }
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) hs_vo[c] = ks.voff[c];
     const int hs_lo = ks.loff[0] * 2;
-    const int hs_oa = ((wave * 64 + r) * OST + 4 * h) * 4;
-    const float hs_nl0 = rowc[0][wave * 64 + r], hs_nl1 = rowc[0][wave * 64 + 32 + r];
-    const float hs_nd0 = -rowc[1][wave * 64 + r], hs_nd1 = -rowc[1][wave * 64 + 32 + r];
+    // the dQ stage address (16x16: row l & 15 of each 16-row block, columns 4 (l >> 4) ..)
+    // and the lane-constant seeds -LSE·log2e, -Δ of the lane's row in each 32-row chain
+    // (16x16: each 16-row block)
+    const int g16 = lane >> 4, i16 = lane & 15;
+    const int hs_sa = ((wave * 64 + r) * OST + 4 * h) * 4;  // (the 32x32 stage address; 'stamps' builds)
+    const int hs_oa = M16 ? ((wave * 64 + i16) * OST + 4 * g16) * 4 : hs_sa;
+    (void)hs_sa;
+    constexpr int NSEED = M16 ? 4 : 2;
+    float hs_nl[NSEED], hs_nd[NSEED];
+#pragma unroll
+    for (int c = 0; c < NSEED; ++c) {
+        const int row = wave * 64 + (M16 ? 16 * c + i16 : 32 * c + r);
+        hs_nl[c] = rowc[0][row];
+        hs_nd[c] = -rowc[1][row];
+    }
+    const float hs_nl0 = hs_nl[0], hs_nl1 = hs_nl[1], hs_nd0 = hs_nd[0], hs_nd1 = hs_nd[1];
     const __amdgpu_buffer_rsrc_t hs_rsk = ks.rs, hs_rsv = vs.rs;
     const int hs_qb = __builtin_amdgcn_readfirstlane(4 * TB * 2 + wave * 64 * D * 2);
     const int hs_db = __builtin_amdgcn_readfirstlane(8 * TB * 2 + wave * 64 * D * 2);
     int hs_cnt = __builtin_amdgcn_readfirstlane(S / KT - 1);
     int hs_goff = __builtin_amdgcn_readfirstlane(KT * D * 4);
+    if constexpr (M16) {
 #ifdef FA2_TILE_BF16
-    asm volatile(FA2_DQ_ASM_D64_BF16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
+        asm volatile(FA2_DQ16_ASM_D64_BF16 : FA2_DQ16_OUTPUTS_D64 : FA2_DQ16_INPUTS_D64 : FA2_DQ16_CLOBBERS_D64);
 #else
-    asm volatile(FA2_DQ_ASM_D64_F16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
+        asm volatile(FA2_DQ16_ASM_D64_F16 : FA2_DQ16_OUTPUTS_D64 : FA2_DQ16_INPUTS_D64 : FA2_DQ16_CLOBBERS_D64);
 #endif
+    } else {
+#ifdef FA2_TILE_BF16
+        asm volatile(FA2_DQ_ASM_D64_BF16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
+#else
+        asm volatile(FA2_DQ_ASM_D64_F16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
+#endif
+    }
     // dQ rows [wave*64 + c*32 + q][OST] (unscaled) -> HBM as whole rows, times 1/sqrt(D)
     constexpr int LPR = D / 4, RPI = 64 / LPR;
     const float dscale = 1.f / __builtin_sqrtf((float)D);
@@ -1769,16 +1811,20 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     int ksp = tune_knob("DQ_KS", 0);
     if constexpr (D == 64) {
         // hand-scheduled kernel (r05): whole 64-key tiles, and a grid of at least one
-        // 256-row workgroup per CU.  DQ_HS (tests and tools): 1 forces it (an error where it
-        // cannot serve), 0 disables it
+        // 256-row workgroup per CU.  DQ_HS (tests and tools): 1 forces it, 2 forces its
+        // 16x16x32 form (A/B; an error where they cannot serve), 0 disables it
         const int hs = tune_knob("DQ_HS", -1);
         const bool fits = S % 64 == 0 && S >= 128;
-        if (hs == 1 && !fits) return hipErrorInvalidValue;
+        if (hs >= 1 && !fits) return hipErrorInvalidValue;
         const long hgrid = (long)bh * ((S + 255) / 256);
-        if (fits && (hs == 1 || (hs < 0 && nw == 0 && ksp == 0 && hgrid >= cu_count()))) {
+        if (fits && (hs >= 1 || (hs < 0 && nw == 0 && ksp == 0 && hgrid >= cu_count()))) {
             if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D>), dim3((unsigned)hgrid), dim3(256), 0, stream, q, k, v,
-                               dout, lse, delta, dq, S, o);
+            if (hs == 2)  // the 16x16x32 loop (A/B and tests)
+                hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D, true>), dim3((unsigned)hgrid), dim3(256), 0, stream,
+                                   q, k, v, dout, lse, delta, dq, S, o);
+            else
+                hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D, false>), dim3((unsigned)hgrid), dim3(256), 0,
+                                   stream, q, k, v, dout, lse, delta, dq, S, o);
             return hipGetLastError();
         }
     }
