@@ -1811,15 +1811,18 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     int ksp = tune_knob("DQ_KS", 0);
     if constexpr (D == 64) {
         // hand-scheduled kernel (r05): whole 64-key tiles, and a grid of at least one
-        // 256-row workgroup per CU.  DQ_HS (tests and tools): 1 forces it, 2 forces its
-        // 16x16x32 form (A/B; an error where they cannot serve), 0 disables it
+        // 256-row workgroup per CU.  DQ_HS (tests and tools): 2 forces it, 1 forces its
+        // 32x32x16 form (A/B; an error where they cannot serve), 0 disables it
         const int hs = tune_knob("DQ_HS", -1);
         const bool fits = S % 64 == 0 && S >= 128;
         if (hs >= 1 && !fits) return hipErrorInvalidValue;
         const long hgrid = (long)bh * ((S + 255) / 256);
         if (fits && (hs >= 1 || (hs < 0 && nw == 0 && ksp == 0 && hgrid >= cu_count()))) {
             if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
-            if (hs == 2)  // the 16x16x32 loop (A/B and tests)
+            // the 16x16x32 loop by default: r05 in-process A/B against the 32x32x16 loop
+            // (DQ_HS = 1): C3 112.7 vs 118.8 us, B2_H8_S4096 99.9 vs 106.0, B16_H16_S2048
+            // 440.5 vs 451.5 (profiles/r05/dq16/)
+            if (hs != 1)
                 hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D, true>), dim3((unsigned)hgrid), dim3(256), 0, stream,
                                    q, k, v, dout, lse, delta, dq, S, o);
             else

@@ -137,14 +137,14 @@ def test_hs_dkdv_deterministic_and_default():
 @pytest.mark.parametrize("form", [1, 2], ids=["m32", "m16"])
 def test_hs_dq_deterministic_and_default(form):
     """bitwise repeatable; at C3's grid the default dQ launch is the hand-scheduled one
-    (DQ_HS = -1 runs the same kernel as DQ_HS = 1, which is checked when form = 1)"""
+    (DQ_HS = -1 runs the same kernel as DQ_HS = 2, the 16x16x32 loop)"""
     B, H, S, D = 4, 16, 2048, 64
     q, k, v = fo.harness_inputs(B, H, S, D, seed=2)
     do = np.random.RandomState(9).randn(B, H, S, D).astype(np.float32)
     tq, tk, tv, tdo = cuda(q, k, v, do)
     o, lse = fa2amd.forward(tq, tk, tv, "fp16")
     res = []
-    for hs in ((-1, 1, 1, 0) if form == 1 else (2, 2, 2, 0)):
+    for hs in ((1, 1, 1, 0) if form == 1 else (-1, 2, 2, 0)):
         fa2amd.tune_set("DQ_HS", hs)
         dq, dk, dv = fa2amd.backward(tq, tk, tv, o, tdo, lse, "fp16")
         torch.cuda.synchronize()
