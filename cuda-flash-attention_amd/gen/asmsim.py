@@ -118,8 +118,12 @@ class Sim:
             for col in range(D):
                 self.lds_write16(2 * (base_halves + tile_off(D, row, col)), int(h[col]))
 
-    def run(self, spike_check=True):
-        D, cfg = self.D, self.cfg
+    def run(self, spike_check=True, m16=False):
+        """fa2_fwd_hs_kernel<D, m16>: the C++ prologue, the asm of fa2_fwd_hs.inc (m16:
+        fa2_fwd16_hs.inc), the C++ epilogue"""
+        import gen_fwd16_hs as G16
+        D = self.D
+        cfg = G16.Cfg(D, self.bf16) if m16 else self.cfg
         TB = 64 * D
         q0 = self.block * 256
         self.stage(self.Q, q0, 256, 4 * TB, np.float32(LOG2E / np.sqrt(D)))
@@ -133,8 +137,12 @@ class Sim:
         ct = 16 * (g & 1) + 4 * (i16 & 3)
         va = [[np.array([2 * tile_off(D, int(rt[l]) + 8 * k, 32 * b + int(ct[l])) for l in lanes]) for k in range(2)]
               for b in range(D // 32)]
+        if m16:
+            ka = [np.array([2 * tile_off(D, int(i16[l]), 32 * ks + 8 * int(g[l])) for l in lanes]) for ks in range(D // 32)]
+            va = [[np.array([2 * tile_off(D, 16 * k + 4 * int(g[l]) + (int(i16[l]) >> 2), 16 * db + 4 * (int(i16[l]) & 3))
+                             for l in lanes]) for k in range(2)] for db in range(D // 16)]
         waves = []
-        text = self.asm_text()
+        text = self.asm_text("fa2_fwd16_hs.inc", "FA2_HS16_ASM") if m16 else self.asm_text()
         for w in range(4):
             tid = 64 * w + lanes
             CPR = D // 8
@@ -147,9 +155,11 @@ class Sim:
                     lo = 2 * np.array([row[l] * D + ((ch[l] ^ SWZ[0](D, int(row[l]))) << 3) for l in lanes])
             ops = {"qb": 4 * TB * 2 + w * 64 * D * 2, "cnt": self.S // 64 - 1, "goff": 64 * D * 4, "flg": 0,
                    "oa": ((w * 64 + r) * cfg.OST + 4 * h) * 4, "lo": lo, "rsk": "K", "rsv": "V"}
-            for t in range(D // 16):
+            if m16:
+                ops["oa"] = ((w * 64 + i16) * cfg.OST + 4 * g) * 4
+            for t in range(len(ka)):
                 ops[f"ka{t}"] = ka[t]
-            for b in range(D // 32):
+            for b in range(len(va)):
                 for k in range(2):
                     ops[f"va{b}_{k}"] = va[b][k]
             for c in range(D // 32):
@@ -170,12 +180,17 @@ class Sim:
         O = np.zeros((256, D), np.float32)
         LSE = np.zeros(256, np.float32)
         for w, wv in enumerate(waves):
-            for c in range(2):
+            for c in range(4 if m16 else 2):
                 l = wv.ops[f"ol{c}"]
-                lt = l[:32] + l[32:]
-                m = wv.ops[f"om{c}"][:32]
-                for q in range(32):
-                    R = w * 64 + c * 32 + q
+                if m16:  # the row's four lane groups
+                    lt = l[:16] + l[16:32] + l[32:48] + l[48:]
+                    m = wv.ops[f"om{c}"][:16]
+                else:
+                    lt = l[:32] + l[32:]
+                    m = wv.ops[f"om{c}"][:32]
+                nr = 16 if m16 else 32
+                for q in range(nr):
+                    R = w * 64 + c * nr + q
                     row = u2f(self.lds[(R * cfg.OST * 4) // 4: (R * cfg.OST * 4) // 4 + D])
                     O[R] = row / lt[q]
                     LSE[R] = m[q] * np.log(2.0) + np.log(lt[q])
@@ -505,6 +520,17 @@ class Wave:
             elif op == "v_accvgpr_write_b32":
                 (f, k), = self.regs(args[0])
                 self.put(f, k, self.vsrc(args[1]))
+            elif op == "v_permlane16_swap_b32":
+                # odd 16-lane rows of the first operand <-> even rows of the second
+                (fa, ka), = self.regs(args[0])
+                (fb, kb), = self.regs(args[1])
+                x, y = self.get(fa, ka).copy(), self.get(fb, kb).copy()
+                x2, y2 = x.copy(), y.copy()
+                for rw in (0, 2):
+                    x2[16 * (rw + 1):16 * (rw + 2)] = y[16 * rw:16 * (rw + 1)]
+                    y2[16 * rw:16 * (rw + 1)] = x[16 * (rw + 1):16 * (rw + 2)]
+                self.put(fa, ka, x2)
+                self.put(fb, kb, y2)
             elif op == "v_permlane32_swap_b32":
                 (fa, ka), = self.regs(args[0])
                 (fb, kb), = self.regs(args[1])
@@ -601,7 +627,7 @@ def main():
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--spike", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", choices=["fwd", "dq", "dq16", "dkdv"], default="fwd")
+    ap.add_argument("--kernel", choices=["fwd", "fwd16", "dq", "dq16", "dkdv"], default="fwd")
     a = ap.parse_args()
     rng = np.random.RandomState(0)
     S, D = a.S, a.D
@@ -649,7 +675,7 @@ def main():
     if a.spike:
         K[S - 3] = 3.0
     sim = Sim(D, a.bf16, S, Q, K, V, a.block)
-    O, LSE, flag, _ = sim.run()
+    O, LSE, flag, _ = sim.run(m16=a.kernel == "fwd16")
     q0 = a.block * 256
     nq = min(256, S - q0)
     s = (Q[q0:q0 + nq].astype(np.float64) @ K.T.astype(np.float64)) / np.sqrt(D)
