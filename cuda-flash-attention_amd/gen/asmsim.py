@@ -118,12 +118,10 @@ class Sim:
             for col in range(D):
                 self.lds_write16(2 * (base_halves + tile_off(D, row, col)), int(h[col]))
 
-    def run(self, spike_check=True, m16=False):
-        """fa2_fwd_hs_kernel<D, m16>: the C++ prologue, the asm of fa2_fwd_hs.inc (m16:
-        fa2_fwd16_hs.inc), the C++ epilogue"""
-        import gen_fwd16_hs as G16
+    def run(self, spike_check=True):
+        """fa2_fwd_hs_kernel<D>: the C++ prologue, the asm of fa2_fwd_hs.inc, the C++ epilogue"""
         D = self.D
-        cfg = G16.Cfg(D, self.bf16) if m16 else self.cfg
+        cfg = self.cfg
         TB = 64 * D
         q0 = self.block * 256
         self.stage(self.Q, q0, 256, 4 * TB, np.float32(LOG2E / np.sqrt(D)))
@@ -137,12 +135,8 @@ class Sim:
         ct = 16 * (g & 1) + 4 * (i16 & 3)
         va = [[np.array([2 * tile_off(D, int(rt[l]) + 8 * k, 32 * b + int(ct[l])) for l in lanes]) for k in range(2)]
               for b in range(D // 32)]
-        if m16:
-            ka = [np.array([2 * tile_off(D, int(i16[l]), 32 * ks + 8 * int(g[l])) for l in lanes]) for ks in range(D // 32)]
-            va = [[np.array([2 * tile_off(D, 16 * k + 4 * int(g[l]) + (int(i16[l]) >> 2), 16 * db + 4 * (int(i16[l]) & 3))
-                             for l in lanes]) for k in range(2)] for db in range(D // 16)]
         waves = []
-        text = self.asm_text("fa2_fwd16_hs.inc", "FA2_HS16_ASM") if m16 else self.asm_text()
+        text = self.asm_text()
         for w in range(4):
             tid = 64 * w + lanes
             CPR = D // 8
@@ -155,8 +149,6 @@ class Sim:
                     lo = 2 * np.array([row[l] * D + ((ch[l] ^ SWZ[0](D, int(row[l]))) << 3) for l in lanes])
             ops = {"qb": 4 * TB * 2 + w * 64 * D * 2, "cnt": self.S // 64 - 1, "goff": 64 * D * 4, "flg": 0,
                    "oa": ((w * 64 + r) * cfg.OST + 4 * h) * 4, "lo": lo, "rsk": "K", "rsv": "V"}
-            if m16:
-                ops["oa"] = ((w * 64 + i16) * cfg.OST + 4 * g) * 4
             for t in range(len(ka)):
                 ops[f"ka{t}"] = ka[t]
             for b in range(len(va)):
@@ -180,17 +172,12 @@ class Sim:
         O = np.zeros((256, D), np.float32)
         LSE = np.zeros(256, np.float32)
         for w, wv in enumerate(waves):
-            for c in range(4 if m16 else 2):
+            for c in range(2):
                 l = wv.ops[f"ol{c}"]
-                if m16:  # the row's four lane groups
-                    lt = l[:16] + l[16:32] + l[32:48] + l[48:]
-                    m = wv.ops[f"om{c}"][:16]
-                else:
-                    lt = l[:32] + l[32:]
-                    m = wv.ops[f"om{c}"][:32]
-                nr = 16 if m16 else 32
-                for q in range(nr):
-                    R = w * 64 + c * nr + q
+                lt = l[:32] + l[32:]
+                m = wv.ops[f"om{c}"][:32]
+                for q in range(32):
+                    R = w * 64 + c * 32 + q
                     row = u2f(self.lds[(R * cfg.OST * 4) // 4: (R * cfg.OST * 4) // 4 + D])
                     O[R] = row / lt[q]
                     LSE[R] = m[q] * np.log(2.0) + np.log(lt[q])
@@ -627,7 +614,7 @@ def main():
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--spike", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", choices=["fwd", "fwd16", "dq", "dq16", "dkdv"], default="fwd")
+    ap.add_argument("--kernel", choices=["fwd", "dq", "dq16", "dkdv"], default="fwd")
     a = ap.parse_args()
     rng = np.random.RandomState(0)
     S, D = a.S, a.D
@@ -675,7 +662,7 @@ def main():
     if a.spike:
         K[S - 3] = 3.0
     sim = Sim(D, a.bf16, S, Q, K, V, a.block)
-    O, LSE, flag, _ = sim.run(m16=a.kernel == "fwd16")
+    O, LSE, flag, _ = sim.run()
     q0 = a.block * 256
     nq = min(256, S - q0)
     s = (Q[q0:q0 + nq].astype(np.float64) @ K.T.astype(np.float64)) / np.sqrt(D)

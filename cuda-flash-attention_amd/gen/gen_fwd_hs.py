@@ -208,11 +208,19 @@ def softmax_part(cfg, c, kb, final):
     for s in range(2):
         for i in range(8 * s, 8 * s + 8):
             out.append(valu(f"v_exp_f32 v{S(i)}, v{S(i)}", [f"v{S(i)}"], [f"v{S(i)}"], kind="exp"))
-        for k in range(4):
-            T = cfg.T(c, k)
-            if kb == 0 and s == 0:
+        if kb == 0 and s == 0:
+            for k in range(4):
+                T = cfg.T(c, k)
                 out.append(valu(f"v_add_f32 v{T}, v{S(k)}, v{S(k + 4)}", [f"v{S(k)}", f"v{S(k + 4)}"], [f"v{T}"]))
-            else:
+        elif "addrr" in asmgen.ABL:
+            # the same sums in the same order per partial, round robin over the partials
+            for e0 in (0, 4):
+                for k in range(4):
+                    T, e = cfg.T(c, k), 8 * s + k + e0
+                    out.append(valu(f"v_add_f32 v{T}, v{T}, v{S(e)}", [f"v{T}", f"v{S(e)}"], [f"v{T}"]))
+        else:
+            for k in range(4):
+                T = cfg.T(c, k)
                 for e in (8 * s + k, 8 * s + k + 4):
                     out.append(valu(f"v_add_f32 v{T}, v{T}, v{S(e)}", [f"v{T}", f"v{S(e)}"], [f"v{T}"]))
         for ii in range(4):

@@ -246,11 +246,6 @@ __device__ __forceinline__ float xor32_sum(float x) {
     const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(s[0]) + __uint_as_float(s[1]);
 }
-// sum over the four 16-lane rows (lanes l, l ^ 16, l ^ 32, l ^ 48)
-__device__ __forceinline__ float xor16_32_sum(float x) {
-    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return xor32_sum(__uint_as_float(s[0]) + __uint_as_float(s[1]));
-}
 
 // ---------------------------------------------------------------------------
 // forward
@@ -820,23 +815,16 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
 #define FA2_HS_INC "fa2_fwd_hs.inc"  // (timing-only ablation builds name another, tools/r05_hs_abl.sh)
 #endif
 #include FA2_HS_INC
-#ifndef FA2_HS16_INC
-#define FA2_HS16_INC "fa2_fwd16_hs.inc"
-#endif
-#include FA2_HS16_INC
 namespace fa2f16 {
 
-// M16: the loop on v_mfma_f32_16x16x32 (fa2_fwd16_hs.inc, gen/gen_fwd16_hs.py): each wave's
-// 64 rows are four 16-row blocks on the lane, a row's keys spread over the four lane groups
-template <int D, bool M16>
+template <int D>
 __global__ void __launch_bounds__(256, 1)
 fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                   float* __restrict__ O, float* __restrict__ LSE, int S) {
     static_assert(D == 64 || D == 128, "hand-scheduled forward: D = 64 or 128");
     constexpr int KT = 64, TB = KT * D;  // halves per tile image
     constexpr int OST = D + 4;           // O stage row stride (floats), as in the generator
-    constexpr int LDSB = M16 ? (D == 64 ? FA2_HS16_LDS_D64 : FA2_HS16_LDS_D128)
-                             : (D == 64 ? FA2_HS_LDS_D64 : FA2_HS_LDS_D128);
+    constexpr int LDSB = D == 64 ? FA2_HS_LDS_D64 : FA2_HS_LDS_D128;
     __shared__ __attribute__((aligned(16))) _Float16 smem[LDSB / 2];
     __shared__ float invl[256];
 
@@ -867,56 +855,25 @@ fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, cons
 
     FragOffsets<D> fo;
     fo.init(lane);
-    // per-lane LDS byte offsets of the row and transposed fragment reads (the 32x32x16 or
-    // the 16x16x32 operand maps: fa2_bwd's FragOffsets16, on this file's swizzle)
-    constexpr int NKA = M16 ? D / 32 : D / 16, NVA = M16 ? D / 16 : D / 32;
-    const int g16 = lane >> 4, i16 = lane & 15;
-    int hs_ka[NKA], hs_va[NVA][2], hs_vo[D / 32];
-    if constexpr (M16) {
+    int hs_ka[D / 16], hs_va[D / 32][2], hs_vo[D / 32];
 #pragma unroll
-        for (int t = 0; t < NKA; ++t) hs_ka[t] = tile_off<D>(i16, 32 * t + 8 * g16) * 2;
+    for (int t = 0; t < D / 16; ++t) hs_ka[t] = fo.row[t] * 2;
 #pragma unroll
-        for (int b = 0; b < NVA; ++b) {
-            hs_va[b][0] = tile_off<D>(4 * g16 + (i16 >> 2), 16 * b + 4 * (i16 & 3)) * 2;
-            hs_va[b][1] = tile_off<D>(16 + 4 * g16 + (i16 >> 2), 16 * b + 4 * (i16 & 3)) * 2;
-        }
-    } else {
-#pragma unroll
-        for (int t = 0; t < NKA; ++t) hs_ka[t] = fo.row[t] * 2;
-#pragma unroll
-        for (int b = 0; b < NVA; ++b) {
-            hs_va[b][0] = fo.tr[b][0] * 2;
-            hs_va[b][1] = fo.tr[b][1] * 2;
-        }
+    for (int b = 0; b < D / 32; ++b) {
+        hs_va[b][0] = fo.tr[b][0] * 2;
+        hs_va[b][1] = fo.tr[b][1] * 2;
     }
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) hs_vo[c] = ks.voff[c];
     const int hs_lo = ks.loff[0] * 2;
-    const int hs_sa = ((wave * 64 + r) * OST + 4 * h) * 4;  // (the 32x32 stage address; 'stamps' builds)
-    const int hs_oa = M16 ? ((wave * 64 + i16) * OST + 4 * g16) * 4 : hs_sa;
-    (void)hs_sa;
+    const int hs_oa = ((wave * 64 + r) * OST + 4 * h) * 4;
     const __amdgpu_buffer_rsrc_t hs_rsk = ks.rs, hs_rsv = vs.rs;
     const int hs_qb = __builtin_amdgcn_readfirstlane(4 * TB * 2 + wave * 64 * D * 2);
     int hs_cnt = __builtin_amdgcn_readfirstlane(S / KT - 1);
     int hs_goff = __builtin_amdgcn_readfirstlane(KT * D * 4);
     float hs_m0, hs_m1, hs_l0, hs_l1;
-    float hs_m[4], hs_l[4];  // M16: per 16-row block (chain c, block qb: 2c + qb)
     unsigned long long hs_flag;
-    if constexpr (M16) {
-        if constexpr (D == 64) {
-#ifdef FA2_TILE_BF16
-            asm volatile(FA2_HS16_ASM_D64_BF16 : FA2_HS16_OUTPUTS_D64 : FA2_HS16_INPUTS_D64 : FA2_HS16_CLOBBERS_D64);
-#else
-            asm volatile(FA2_HS16_ASM_D64_F16 : FA2_HS16_OUTPUTS_D64 : FA2_HS16_INPUTS_D64 : FA2_HS16_CLOBBERS_D64);
-#endif
-        } else {
-#ifdef FA2_TILE_BF16
-            asm volatile(FA2_HS16_ASM_D128_BF16 : FA2_HS16_OUTPUTS_D128 : FA2_HS16_INPUTS_D128 : FA2_HS16_CLOBBERS_D128);
-#else
-            asm volatile(FA2_HS16_ASM_D128_F16 : FA2_HS16_OUTPUTS_D128 : FA2_HS16_INPUTS_D128 : FA2_HS16_CLOBBERS_D128);
-#endif
-        }
-    } else if constexpr (D == 64) {
+    if constexpr (D == 64) {
 #ifdef FA2_TILE_BF16
         asm volatile(FA2_HS_ASM_D64_BF16 : FA2_HS_OUTPUTS_D64 : FA2_HS_INPUTS_D64 : FA2_HS_CLOBBERS_D64);
 #else
@@ -932,26 +889,14 @@ fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, cons
 
     if (!__syncthreads_or(hs_flag != 0)) {
         // O rows [wave*64 + c*32 + q][OST] (unnormalised) are in the stage; l is per lane
-        // half (M16: per lane group): the xor sum is the row's total
-        if constexpr (M16) {
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const float lt = xor16_32_sum(hs_l[b]);
-                if (g16 == 0) {
-                    invl[wave * 64 + 16 * b + i16] = 1.f / lt;
-                    const int q = qrow0 + wave * 64 + 16 * b + i16;
-                    if (q < S) LSE[(long)bh * S + q] = hs_m[b] * FA2_LN2 + __logf(lt);
-                }
-            }
-        } else {
-            const float lt0 = xor32_sum(hs_l0), lt1 = xor32_sum(hs_l1);
-            if (h == 0) {
-                invl[wave * 64 + r] = 1.f / lt0;
-                invl[wave * 64 + 32 + r] = 1.f / lt1;
-                const int q0 = qrow0 + wave * 64 + r;
-                if (q0 < S) LSE[(long)bh * S + q0] = hs_m0 * FA2_LN2 + __logf(lt0);
-                if (q0 + 32 < S) LSE[(long)bh * S + q0 + 32] = hs_m1 * FA2_LN2 + __logf(lt1);
-            }
+        // half: the xor-32 sum is the row's total
+        const float lt0 = xor32_sum(hs_l0), lt1 = xor32_sum(hs_l1);
+        if (h == 0) {
+            invl[wave * 64 + r] = 1.f / lt0;
+            invl[wave * 64 + 32 + r] = 1.f / lt1;
+            const int q0 = qrow0 + wave * 64 + r;
+            if (q0 < S) LSE[(long)bh * S + q0] = hs_m0 * FA2_LN2 + __logf(lt0);
+            if (q0 + 32 < S) LSE[(long)bh * S + q0 + 32] = hs_m1 * FA2_LN2 + __logf(lt1);
         }
         __builtin_amdgcn_wave_barrier();
         // whole rows: D/4 lanes per row, 16-B pieces
@@ -1083,15 +1028,10 @@ static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v,
 
 template <int D>
 static hipError_t fwd_hs_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
-                                hipStream_t stream, bool m16) {
+                                hipStream_t stream) {
     const long grid = (long)bh * ((S + 255) / 256);
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    if (m16)
-        hipLaunchKernelGGL((fa2f16::fa2_fwd_hs_kernel<D, true>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, o,
-                           lse, S);
-    else
-        hipLaunchKernelGGL((fa2f16::fa2_fwd_hs_kernel<D, false>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v,
-                           o, lse, S);
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_hs_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, o, lse, S);
     return hipGetLastError();
 }
 
@@ -1101,14 +1041,16 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     if constexpr (D == 64 || D == 128) {
         // hand-scheduled kernel (r05): full 64-key tiles only, and a grid of at least one
         // 256-row workgroup per CU (smaller grids keep the key-split plans below).
-        // FWD_HS (tests and tools): 1 forces it, 2 its 16x16x32 loop (an error where they
-        // cannot serve), 0 disables it
+        // FWD_HS (tests and tools): 1 forces it (an error where it cannot serve), 0 disables it.
+        // (Its 16x16x32 form lost in r05: C3 +3.6 %, B2_H8_S4096 +4.7 %, C4 +0.8 %, in-process,
+        // profiles/r05/fwd16/: the forward is issue-bound and 16x16x32 halves the issue room
+        // per MFMA cycle)
         const int hs = tune_knob("FWD_HS", -1);
         const bool fits = S % 64 == 0 && S >= 128;
-        if (hs >= 1 && !fits) return hipErrorInvalidValue;
+        if (hs == 1 && !fits) return hipErrorInvalidValue;
         const bool forced_other = tune_knob("FWD_WAVES", 0) || tune_knob("FWD_KS", 0) || tune_knob("FWD_NKB", 0);
-        if (fits && (hs >= 1 || (hs < 0 && !forced_other && (long)bh * ((S + 255) / 256) >= cu_count())))
-            return fwd_hs_launch<D>(q, k, v, o, lse, bh, S, stream, hs == 2);
+        if (fits && (hs == 1 || (hs < 0 && !forced_other && (long)bh * ((S + 255) / 256) >= cu_count())))
+            return fwd_hs_launch<D>(q, k, v, o, lse, bh, S, stream);
     }
     // 8 waves (2 per SIMD) where the registers allow it; D = 128 runs 4 waves of
     // ~400 VGPRs (8 would spill and exceed the LDS budget with the Q stages)

@@ -30,18 +30,10 @@ def test_forward_loop(D, S, bf16):
     assert "restart flag False" in out
 
 
-@pytest.mark.parametrize("D,S,bf16", [(64, 256, False), (64, 192, True), (128, 192, False), (128, 320, True)])
-def test_forward16_loop(D, S, bf16):
-    """the 16x16x32 form of the forward loop"""
-    out = sim("--kernel", "fwd16", "--D", str(D), "--S", str(S), *(["--bf16"] if bf16 else []))
-    assert "restart flag False" in out
-
-
-@pytest.mark.parametrize("kernel", ["fwd", "fwd16"])
 @pytest.mark.parametrize("D", [64, 128])
-def test_forward_loop_flags_a_late_spike(D, kernel):
+def test_forward_loop_flags_a_late_spike(D):
     """a late key far above the first tile's row max must raise the restart flag"""
-    assert "restart flag True" in sim("--kernel", kernel, "--D", str(D), "--S", "256", "--spike")
+    assert "restart flag True" in sim("--kernel", "fwd", "--D", str(D), "--S", "256", "--spike")
 
 
 @pytest.mark.parametrize("S,block", [(128, 0), (192, 0), (256, 0), (512, 1)])
@@ -61,7 +53,7 @@ def test_dkdv_loop(S, block, bf16):
     sim("--kernel", "dkdv", "--D", "64", "--S", str(S), "--block", str(block), *(["--bf16"] if bf16 else []))
 
 
-@pytest.mark.parametrize("gen", ["gen_fwd_hs.py", "gen_fwd16_hs.py", "gen_bwd_dq.py", "gen_bwd_dq16.py", "gen_bwd_dkdv.py"])
+@pytest.mark.parametrize("gen", ["gen_fwd_hs.py", "gen_bwd_dq.py", "gen_bwd_dq16.py", "gen_bwd_dkdv.py"])
 def test_generated_loops_are_current(gen):
     """each committed kernels/*.inc is what its generator writes from its current source"""
     r = subprocess.run([sys.executable, os.path.join(GEN, gen), "--check"], capture_output=True, text=True,

@@ -16,7 +16,6 @@ for spec in "$@"; do
     dq)   G=gen_bwd_dq.py;   M=FA2_DQ_INC; rm -f "$D"/build/f-attn2-backward_f16.o "$D"/build/f-attn2-backward_bf16.o ;;
     dkdv) G=gen_bwd_dkdv.py; M=FA2_DK_INC; rm -f "$D"/build/f-attn2-backward_f16.o "$D"/build/f-attn2-backward_bf16.o ;;
     dq16) G=gen_bwd_dq16.py; M=FA2_DQ16_INC; rm -f "$D"/build/f-attn2-backward_f16.o "$D"/build/f-attn2-backward_bf16.o ;;
-    fwd16) G=gen_fwd16_hs.py; M=FA2_HS16_INC; rm -f "$D"/build/kernel_fa2_optimized_f16.o "$D"/build/kernel_fa2_optimized_bf16.o ;;
   esac
   python3 "$P/gen/$G" --abl "$A" --out "$D/abl.inc" > /dev/null
   make -s -j8 -C "$P" lib BUILD="$D/build" LIBDIR="$D" EXTRA="-D$M=\\\"$D/abl.inc\\\""
