@@ -8,15 +8,18 @@ C++ epilogue (dK, dV rows from an LDS stage; dK times 1/sqrt(D)).  The math is t
 part of the reference's backward (kernels/f-attn2-backward_f16.cu:170-268):
 P = exp(Q K^T / sqrt(D) - LSE), dV = P^T dO, dS = P o (dO V^T - Delta), dK = dS^T Q / sqrt(D):
 
-  * one workgroup = 4 waves = 256 keys, ONE wave per SIMD; each wave holds 64 keys as two
-    32-key chains A and B: their K and V fragments and dK^T / dV^T accumulators sit in
-    AGPRs for the whole query loop;
+  * one workgroup = 4 waves = 256 keys, ONE wave per SIMD; each wave holds 64 keys (two
+    32-key blocks kb): their K and V fragments and dK^T / dV^T accumulators sit in AGPRs
+    for the whole query loop;
   * the head's queries stream in 64-row steps (Q and dO as fp16/bf16 tiles, -LSE*log2e and
-    -Delta rows) through a 3-slot LDS ring, one barrier per step; per step four phases:
-        P1  S, dP of A (step j)        | P, dS of B (step j-1), query block 1
-        P2  dV^T, dK^T of B (step j-1)| P, dS of A (step j),   query block 0
-        P3  S, dP of B (step j)        | P, dS of A (step j),   query block 1   -> barrier
-        P4  dV^T, dK^T of A (step j)  | P, dS of B (step j),   query block 0
+    -Delta rows) through a 3-slot LDS ring, one barrier per step.  The step's two 32-row
+    query blocks are the two chains A and B (r05: chains split by query, not by key, so
+    every transposed dO^T / Q^T fragment and every row-constant tuple is read once per
+    step, by the one chain it belongs to); per step four phases:
+        P1  S, dP of A (step j)        | P, dS of B (step j-1), key block 1
+        P2  dV^T, dK^T of B (step j-1)| P, dS of A (step j),   key block 0
+        P3  S, dP of B (step j)        | P, dS of A (step j),   key block 1   -> barrier
+        P4  dV^T, dK^T of A (step j)  | P, dS of B (step j),   key block 0
   * S = Q K^T starts from -LSE*log2e and dP = dO V^T from -Delta (16-register row-constant
     tuples read from LDS into a 2-slot ring: the query is on the accumulator rows), so
     P = exp2(acc) and dS = P * acc; P and dS are packed in place and ARE the B operands
@@ -26,11 +29,12 @@ P = exp(Q K^T / sqrt(D) - LSE), dV = P^T dO, dS = P o (dO V^T - Delta), dK = dS^
     their use; the row constants by one dword load per lane of waves 0 (LSE) and 1 (Delta).
 
 Register map (D = 64):
-  AGPR  dK^T[c][b] a[16(2c+b)]    dV^T[c][b] a[64+16(2c+b)]
-        K[c][t]    a[128+4(4c+t)] V[c][t]    a[160+4(4c+t)]
+  AGPR  dK^T[kb][b] a[16(2kb+b)]  dV^T[kb][b] a[64+16(2kb+b)]
+        K[kb][t]   a[128+4(4kb+t)] V[kb][t]  a[160+4(4kb+t)]
         Q rows     a[192+4(4qb+t)] dO rows   a[224+4(4qb+t)]
-  VGPR  S[c][qb]   v[32c+16qb]    dP[c][qb]  v[64+32c+16qb]
-        seed ring  v[128..159]    trop ring  v[160..191]   staging v[192..223]  row const v[224]
+  VGPR  S[qb][kb]  v[32qb+16kb]   dP[qb][kb] v[64+32qb+16kb]   (qb = the chain)
+        seed ring  v[128..159] (the chain's -LSE*log2e, -Delta tuples)
+        trop ring  v[160..191] (the chain's 8 dO^T / Q^T fragments)   staging v[192..223]  row const v[224]
 
 Usage: python3 gen_bwd_dkdv.py [--check]
 """
@@ -82,11 +86,11 @@ class Cfg:
         return 224 + 4 * (4 * qb + t)
 
     # VGPRs
-    def S(self, c, qb, i=0):
-        return 32 * c + 16 * qb + i
+    def S(self, qb, kb, i=0):
+        return 32 * qb + 16 * kb + i
 
-    def dP(self, c, qb, i=0):
-        return 64 + 32 * c + 16 * qb + i
+    def dP(self, qb, kb, i=0):
+        return 64 + 32 * qb + 16 * kb + i
 
     def seed(self, k):
         return 128 + 16 * k
@@ -140,18 +144,17 @@ def seed_reads(cfg, slot, which, qb, k, earliest=0, deadline=None):
 
 
 def trop_frag(cfg, k):
-    """the k-th A operand of a dV^T / dK^T phase: (tensor, b, qb, s)"""
-    b, rest = k // 8, k % 8
-    tensor = rest // 4  # 0: dO^T (for dV), 1: Q^T (for dK)
-    qb, s = (rest % 4) // 2, rest % 2
-    return tensor, b, qb, s
+    """the k-th A operand of a chain's dV^T / dK^T phase: (tensor, b, s)"""
+    tensor = k // 4  # 0: dO^T (for dV), 1: Q^T (for dK)
+    b, s = (k % 4) // 2, k % 2
+    return tensor, b, s
 
 
-def trop_reads(cfg, slot, k, earliest=0, deadline=None):
-    tensor, b, qb, s = trop_frag(cfg, k)
+def trop_reads(cfg, slot, qb, k, earliest=0, deadline=None):
+    tensor, b, s = trop_frag(cfg, k)
     tt = 1 if tensor == 0 else 0  # LDS tile: 0 = Q, 1 = dO
     off = slot * cfg.SLOT + tt * cfg.TBB + (qb * 32 + 16 * s) * cfg.D * 2
-    d = cfg.tr(k % 8)
+    d = cfg.tr(k)
     return tagged("lds", [
         Ins(f"ds_read_b64_tr_b16 {rtxt('v', d, 2)}, %[tr{b}_0] offset:{off}", "dsr", [], rng("v", d, 2),
             earliest=earliest, deadline=deadline),
@@ -160,48 +163,51 @@ def trop_reads(cfg, slot, k, earliest=0, deadline=None):
 
 
 # ---- MFMA chains -------------------------------------------------------------------------
-SEED_ORDER = [(0, 0, 0), (1, 0, 1), (0, 1, 0), (1, 1, 1)]  # (which, qb, ring slot) in MFMA order
+SEED_ORDER = [(0, 0, 0), (1, 0, 1), (0, 1, 0), (1, 1, 1)]  # (which, kb, seed ring slot) in MFMA order
 
 
-def sdp_mfmas(cfg, c):
-    """S[c][qb] = Q K^T - LSE*log2e, dP[c][qb] = dO V^T - Delta: S qb0, dP qb0, S qb1, dP qb1"""
+def sdp_mfmas(cfg, qb):
+    """chain qb: S[qb][kb] = Q K^T - LSE*log2e, dP[qb][kb] = dO V^T - Delta; S kb0, dP kb0, S kb1,
+    dP kb1 (key block 0 first: its P, dS are the next phase's filler)"""
     out = []
-    for which, qb, k in SEED_ORDER:
+    for which, kb, k in SEED_ORDER:
         for t in range(cfg.NTQ):
             if which == 0:
-                dst, a, b = cfg.S(c, qb), cfg.Qr(qb, t), cfg.Kf(c, t)
+                dst, a, b = cfg.S(qb, kb), cfg.Qr(qb, t), cfg.Kf(kb, t)
             else:
-                dst, a, b = cfg.dP(c, qb), cfg.dOr(qb, t), cfg.Vf(c, t)
+                dst, a, b = cfg.dP(qb, kb), cfg.dOr(qb, t), cfg.Vf(kb, t)
             cc = ("v", cfg.seed(k)) if t == 0 else ("v", dst)
             out.append(mfma(cfg, ("v", dst), ("a", a), ("a", b), cc))
     return out
 
 
-def dkdv_mfmas(cfg, c, first=False):
-    """dV^T[c][b] += dO^T P[c], dK^T[c][b] += Q^T dS[c]; the k-th MFMA takes trop ring slot k % 8"""
+def dkdv_mfmas(cfg, qb, first=False):
+    """chain qb's share: dV^T[kb][b] += dO^T P[qb][kb], dK^T[kb][b] += Q^T dS[qb][kb]; trop ring
+    slot k (fragment k of the chain) feeds the two key blocks back to back"""
     out = []
-    for k in range(16):
-        tensor, b, qb, s = trop_frag(cfg, k)
-        acc = cfg.dV(c, b) if tensor == 0 else cfg.dK(c, b)
-        src = cfg.S(c, qb, 8 * s) if tensor == 0 else cfg.dP(c, qb, 8 * s)
-        z = first and qb == 0 and s == 0
-        out.append(mfma(cfg, ("a", acc), ("v", cfg.tr(k % 8)), ("v", src), ("a", acc), c_is_zero=z))
+    for k in range(8):
+        tensor, b, s = trop_frag(cfg, k)
+        for kb in range(2):
+            acc = cfg.dV(kb, b) if tensor == 0 else cfg.dK(kb, b)
+            src = cfg.S(qb, kb, 8 * s) if tensor == 0 else cfg.dP(qb, kb, 8 * s)
+            z = first and s == 0
+            out.append(mfma(cfg, ("a", acc), ("v", cfg.tr(k)), ("v", src), ("a", acc), c_is_zero=z))
     return out
 
 
 # ---- VALU ---------------------------------------------------------------------------------
-def pds_part(cfg, c, qb):
-    """P = exp2(S) and dS = P * dP' of query block qb of chain c, packed in place"""
+def pds_part(cfg, qb, kb):
+    """P = exp2(S) and dS = P * dP' of key block kb of chain qb, packed in place"""
     out = []
     for s in range(2):
         g0 = 8 * s
         for i in range(g0, g0 + 8):
-            r = cfg.S(c, qb, i)
+            r = cfg.S(qb, kb, i)
             out.append(valu(f"v_exp_f32 v{r}, v{r}", [f"v{r}"], [f"v{r}"], kind="exp"))
         for i in range(g0, g0 + 8):
-            r, d = cfg.S(c, qb, i), cfg.dP(c, qb, i)
+            r, d = cfg.S(qb, kb, i), cfg.dP(qb, kb, i)
             out.append(valu(f"v_mul_f32 v{d}, v{d}, v{r}", [f"v{d}", f"v{r}"], [f"v{d}"]))
-        for base in (cfg.S(c, qb, g0), cfg.dP(c, qb, g0)):
+        for base in (cfg.S(qb, kb, g0), cfg.dP(qb, kb, g0)):
             for ii in range(4):
                 d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
                 out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
@@ -248,45 +254,37 @@ def body(cfg, j3, log):
     chain B's dV/dK of step j-1 read slot (j3+2)%3"""
     s, n, pv = j3, (j3 + 1) % 3, (j3 + 2) % 3
     seq = []
-    # P1: S, dP of A | P, dS of B (j-1) qb 1; seeds qb 1; stage step j+1; trop 0..7 for P2
-    sd = seed_reads(cfg, s, 0, 1, 0, earliest=2, deadline=5) + seed_reads(cfg, s, 1, 1, 1, earliest=6, deadline=9)
+    # P1: S, dP of A | P, dS of B (j-1) key block 1; stage step j+1; B's (j-1) trop frags for P2
     pre = []
     for k in range(8):
-        pre += trop_reads(cfg, pv, k, earliest=8)
+        pre += trop_reads(cfg, pv, 1, k, earliest=2)
     conv = staging_convert(cfg, n)
     for i in conv:
         i.earliest = 2
-    seq += schedule_phase(cfg, sdp_mfmas(cfg, 0), [pds_part(cfg, 1, 1), sd, conv, pre], f"P1.{j3}", log)
-    # P2: dV, dK of B (j-1) | P, dS of A qb 0; trop 8..15; seeds qb 0 for P3; loads of step j+2
-    tr = []
-    for k in range(8, 16):
-        tr += trop_reads(cfg, pv, k, earliest=k - 8 + 2, deadline=k - 3)
-    sd = seed_reads(cfg, s, 0, 0, 0) + seed_reads(cfg, s, 1, 0, 1)
-    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 1), [pds_part(cfg, 0, 0), tr, sd, staging_loads(cfg)], f"P2.{j3}",
-                          log)
-    # P3: S, dP of B | P, dS of A qb 1; seeds qb 1; trop 0..7 for P4
-    sd = seed_reads(cfg, s, 0, 1, 0, earliest=2, deadline=5) + seed_reads(cfg, s, 1, 1, 1, earliest=6, deadline=9)
+    seq += schedule_phase(cfg, sdp_mfmas(cfg, 0), [pds_part(cfg, 1, 1), conv, pre], f"P1.{j3}", log)
+    # P2: dV, dK of B (j-1) | P, dS of A key block 0; seeds of B for P3 (A's done with the ring);
+    #     loads of step j+2
+    sd = seed_reads(cfg, s, 0, 1, 0) + seed_reads(cfg, s, 1, 1, 1)
+    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 1), [pds_part(cfg, 0, 0), sd, staging_loads(cfg)], f"P2.{j3}", log)
+    # P3: S, dP of B | P, dS of A key block 1; A's trop frags for P4 (the ring is free after P2)
     pre = []
     for k in range(8):
-        pre += trop_reads(cfg, s, k, earliest=8)
-    seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [pds_part(cfg, 0, 1), sd, pre], f"P3.{j3}", log)
+        pre += trop_reads(cfg, s, 0, k)
+    seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [pds_part(cfg, 0, 1), pre], f"P3.{j3}", log)
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     seq.append(tagged("bar", [Ins("s_barrier", "bar")])[0])
-    # P4: dV, dK of A | P, dS of B qb 0; trop 8..15; Q/dO rows and seeds qb 0 of step j+1
-    tr = []
-    for k in range(8, 16):
-        tr += trop_reads(cfg, s, k, earliest=k - 8 + 2, deadline=k - 3)
-    nxt = rowop_reads(cfg, n) + seed_reads(cfg, n, 0, 0, 0) + seed_reads(cfg, n, 1, 0, 1)
-    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 0), [pds_part(cfg, 1, 0), tr, nxt], f"P4.{j3}", log)
+    # P4: dV, dK of A | P, dS of B key block 0; Q/dO rows and A's seeds of step j+1 (the seed
+    #     ring is free after P3)
+    nxt = rowop_reads(cfg, n) + seed_reads(cfg, n, 0, 0, 0, earliest=2) + seed_reads(cfg, n, 1, 0, 1, earliest=2)
+    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 0), [pds_part(cfg, 1, 0), nxt], f"P4.{j3}", log)
     return seq
 
 
 def prologue(cfg):
-    """step 0 serially (both chains' S, dP; A's P, dS and dV, dK; B's first half), step 1 staged"""
+    """step 0 serially (both chains' S, dP; A's P, dS and dV, dK -- whose first MFMAs start
+    every accumulator from zero; B's first half), step 1 staged"""
     D, NTQ = cfg.D, cfg.NTQ
-    seq = [valu(f"v_accvgpr_write_b32 a{cfg.dK(1, 0) + i}, 0", [], [f"a{cfg.dK(1, 0) + i}"]) for i in range(32)]
-    seq += [valu(f"v_accvgpr_write_b32 a{cfg.dV(1, 0) + i}, 0", [], [f"a{cfg.dV(1, 0) + i}"]) for i in range(32)]
-    seq += staging_loads(cfg)  # step 1
+    seq = staging_loads(cfg)  # step 1
     # K and V fragments of both chains from the workgroup's K / V blocks (%[kvb]: this wave's rows)
     for t in range(NTQ):
         seq.append(valu(f"v_add_u32 v{t}, %[kvb], %[ka{t}]", [], [f"v{t}"]))
@@ -297,21 +295,14 @@ def prologue(cfg):
             seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.Vf(c, t), 4)}, v{t} offset:{KEYS * D * 2 + c * 32 * D * 2}",
                            "dsr", R([f"v{t}"]), rng("a", cfg.Vf(c, t), 4)))
     seq += rowop_reads(cfg, 0)
-    for c in range(2):
-        for which, qb, k in SEED_ORDER:
-            seq += seed_reads(cfg, 0, which, qb, k)
-            for t in range(NTQ):
-                if which == 0:
-                    dst, a, b = cfg.S(c, qb), cfg.Qr(qb, t), cfg.Kf(c, t)
-                else:
-                    dst, a, b = cfg.dP(c, qb), cfg.dOr(qb, t), cfg.Vf(c, t)
-                cc = ("v", cfg.seed(k)) if t == 0 else ("v", dst)
-                seq.append(mfma(cfg, ("v", dst), ("a", a), ("a", b), cc))
+    for qb in range(2):
+        seq += seed_reads(cfg, 0, 0, qb, 0) + seed_reads(cfg, 0, 1, qb, 1)
+        seq += sdp_mfmas(cfg, qb)
     seq += pds_part(cfg, 0, 0) + pds_part(cfg, 0, 1) + pds_part(cfg, 1, 0)
     mf = dkdv_mfmas(cfg, 0, first=True)
-    for k in range(16):
-        seq += trop_reads(cfg, 0, k)
-        seq.append(mf[k])
+    for k in range(8):
+        seq += trop_reads(cfg, 0, 0, k)
+        seq += mf[2 * k:2 * k + 2]
     seq += staging_convert(cfg, 1)
     seq += staging_loads(cfg)  # step 2
     seq += [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_barrier", "bar")]
@@ -325,12 +316,12 @@ def epilogue(cfg, last_slot_expr):
     seq = [Ins("s_waitcnt vmcnt(0) lgkmcnt(0)", "wait")]
     seq += pds_part(cfg, 1, 1)
     mf = dkdv_mfmas(cfg, 1)
-    for k in range(16):
-        seq += trop_reads(cfg, last_slot_expr, k)
-        seq.append(mf[k])
+    for k in range(8):
+        seq += trop_reads(cfg, last_slot_expr, 1, k)
+        seq += mf[2 * k:2 * k + 2]
     seq.append(Ins("s_barrier", "bar"))
     for tensor, op in ((0, "%[oak]"), (1, "%[oav]")):
-        for c in range(2):
+        for c in range(2):  # key block
             for b in range(cfg.NB):
                 for g in range(4):
                     r = (cfg.dK(c, b) if tensor == 0 else cfg.dV(c, b)) + 4 * g
