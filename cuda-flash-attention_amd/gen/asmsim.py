@@ -183,14 +183,13 @@ class Sim:
                     LSE[R] = m[q] * np.log(2.0) + np.log(lt[q])
         return O, LSE, flag, waves
 
-    def run_dq(self, dO, LSE, Delta, m16=False):
-        """fa2_bwd_dq_hs_kernel<64, m16>: the C++ prologue, the asm of fa2_bwd_dq_hs.inc
-        (m16: fa2_bwd_dq16_hs.inc), the dQ rows"""
+    def run_dq(self, dO, LSE, Delta):
+        """fa2_bwd_dq_hs_kernel<64>: the C++ prologue, the asm of fa2_bwd_dq_hs.inc, the dQ rows"""
         import gen_bwd_dq as GD
-        import gen_bwd_dq16 as GD16
         SWZ[0] = swz_bwd
         D = self.D
-        cfg = (GD16 if m16 else GD).Cfg(D, self.bf16)
+        cfg = GD.Cfg(D, self.bf16)
+        m16 = True
         TB = 64 * D
         self.lds = np.zeros(cfg.lds_bytes // 4, np.uint32)
         q0 = self.block * 256
@@ -210,8 +209,7 @@ class Sim:
             ka = [np.array([2 * tile_off(D, int(i16[l]), 32 * ks + 8 * int(g[l])) for l in lanes]) for ks in range(D // 32)]
             kt = [[np.array([2 * tile_off(D, 16 * k + 4 * int(g[l]) + (int(i16[l]) >> 2), 16 * db + 4 * (int(i16[l]) & 3))
                              for l in lanes]) for k in range(2)] for db in range(D // 16)]
-        text = self.asm_text("fa2_bwd_dq16_hs.inc", "FA2_DQ16_ASM") if m16 else \
-            self.asm_text("fa2_bwd_dq_hs.inc", "FA2_DQ_ASM")
+        text = self.asm_text("fa2_bwd_dq_hs.inc", "FA2_DQ_ASM")
         waves = []
         for w in range(4):
             tid = 64 * w + lanes
@@ -614,7 +612,7 @@ def main():
     ap.add_argument("--bf16", action="store_true")
     ap.add_argument("--spike", action="store_true")
     ap.add_argument("--block", type=int, default=0)
-    ap.add_argument("--kernel", choices=["fwd", "dq", "dq16", "dkdv"], default="fwd")
+    ap.add_argument("--kernel", choices=["fwd", "dq", "dkdv"], default="fwd")
     a = ap.parse_args()
     rng = np.random.RandomState(0)
     S, D = a.S, a.D
@@ -640,7 +638,7 @@ def main():
         tol = 2e-2 if a.bf16 else 1e-2
         assert ek < tol and ev < tol, "mismatch"
         return
-    if a.kernel in ("dq", "dq16"):
+    if a.kernel == "dq":
         dO = rng.randn(S, D).astype(np.float32)
         s64 = (Q.astype(np.float64) @ K.T.astype(np.float64)) / np.sqrt(D)
         mx = s64.max(1, keepdims=True)
@@ -651,7 +649,7 @@ def main():
         dS = P * (dO.astype(np.float64) @ V.T.astype(np.float64) - delta[:, None])
         edq = dS @ K.astype(np.float64) / np.sqrt(D)
         sim = Sim(D, a.bf16, S, Q, K, V, a.block)
-        dq = sim.run_dq(dO, lse.astype(np.float32), delta.astype(np.float32), m16=a.kernel == "dq16")
+        dq = sim.run_dq(dO, lse.astype(np.float32), delta.astype(np.float32))
         q0 = a.block * 256
         nq = min(256, S - q0)
         err = np.abs(dq[:nq] - edq[q0:q0 + nq]).max()

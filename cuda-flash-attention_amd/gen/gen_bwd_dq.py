@@ -14,23 +14,37 @@ query row (no atomics), the three products per tile on MFMA:
     in AGPRs for the whole key loop;
   * per 64-key tile four phases, each one MFMA chain with the other chain's VALU placed in
     its gaps (gen_fwd_hs.py's structure, with S^T and dP^T together as the first chain):
-        P1  S^T, dP^T of A (tile j)   | dS of B (tile j-1), scores 8..31
-        P2  dQ^T of B (tile j-1)      | dS of A (tile j),   scores 0..7
-        P3  S^T, dP^T of B (tile j)   | dS of A (tile j),   scores 8..31   -> barrier
-        P4  dQ^T of A (tile j)        | dS of B (tile j),   scores 0..7
-    (the dS work is split 8 / 24 of each lane's 32 scores so the short dQ phases, 8 MFMAs, and
-    the long ones, 16, carry issue in proportion);
+        P1  S^T, dP^T of A (tile j)   | dS of B (tile j-1), three quarters
+        P2  dQ^T of B (tile j-1)      | dS of A (tile j),   the first quarter
+        P3  S^T, dP^T of B (tile j)   | dS of A (tile j),   three quarters   -> barrier
+        P4  dQ^T of A (tile j)        | dS of B (tile j),   the first quarter
   * S^T = K Q^T starts from -LSE*log2e and dP^T = V dO^T from -Delta (lane-constant splats:
     the query is on the lane), so P = exp2(acc) and dS = P * acc, one v_exp and one v_mul
     per score; dS is packed to fp16/bf16 in place and IS the B operand of
     dQ^T += K^T dS^T (K^T through ds_read_b64_tr_b16 of the K tile);
-  * K and V tiles: fp32 HBM -> registers -> fp16/bf16 -> swizzled LDS, one tile ahead.
+  * K and V tiles: fp32 HBM -> registers -> fp16/bf16 -> swizzled LDS, one tile ahead;
+  * all on v_mfma_f32_16x16x32 (r05: 5-6 % faster than the same loop on 32x32x16 at C3 and
+    B2_H8_S4096 in-process, profiles/r05/dq16/ -- less energy per FLOP at the power cap,
+    where the kernel runs), on the operand maps:
 
-Register map (D = 64):
-  AGPR  dQ^T[c][b]  a[16(2c+b)]    Q[c][t] a[64+4(4c+t)]   dO[c][t] a[96+4(4c+t)]
-        K^T frags   a[128+4i]      K rows  a[160+4f]       V rows   a[192+4f]
-  VGPR  S^T[c][kb]  v[32c+16kb]    dP^T[c][kb] v[64+32c+16kb]
-        -LSE splat  v[128+16c]     -Delta splat v[160+16c]   staging v[192..223]
+  A[m = l & 15][k = 8g + j], B[k = 8g + j][n = l & 15], C[m = 4g + i][n = l & 15]  (g = l >> 4)
+
+  * S^T / dP^T tiles [16 keys][16 queries]: A = K / V row fragments (rows 16 kb + (l & 15),
+    columns 32 ks + 8g), B = Q / dO fragments of the wave's query block (query on the lane);
+    the first MFMA of each tile starts from the -LSE*log2e / -Delta splat of its query block;
+  * dQ^T[16 d][16 q] += K^T dS^T over 32 keys per MFMA: B = the packed dS of two key blocks,
+    k-slot 8g + j <-> key 16 (j >> 2) + 4g + (j & 3) of the 32; A = K^T by two 4-row
+    transposed reads (rows 4g.. and 16 + 4g.., columns 16 db ..) in the same key order.
+
+16x16x32 reads and writes a quarter of the accumulator per instruction for half the FLOPs,
+and the splat seeds are 4 registers per 16-query block.
+
+Register map (D = 64; c chain, qb its 16-row query blocks, kb 16-key blocks, ks / s 32-steps):
+  AGPR  dQ^T[c][db][qb] a[32c + 8db + 4qb]   Q[c][qb][ks] a[64 + 16c + 8qb + 4ks]
+        dO[c][qb][ks]   a[96 + ...]           K^T[db][s] a[128 + 4(2db + s)]
+        K rows[kb][ks]  a[160 + 4(2kb + ks)]  V rows[kb][ks] a[192 + 4(2kb + ks)]
+  VGPR  S^T[c][qb][kb]  v[32c + 16qb + 4kb]   dP^T v[64 + ...]
+        -LSE splat[c][qb] v[128 + 4(2c + qb)] -Delta splat v[144 + ...]  staging v[160..191]
 
 Usage: python3 gen_bwd_dq.py [--check]
 """
@@ -43,63 +57,63 @@ from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng,
 
 KT = 64
 ROWS = 256
-# dS work per chain and tile = 4 groups of 8 scores (kb, first score); the first part (in the
-# short dQ phase) takes one group, the second part (in the long S^T/dP^T phase) three
+# dS groups per chain and tile: (qb, s) = 8 scores of each lane (key blocks 2s, 2s+1 of
+# query block qb); the first part (in the short dQ phase) takes one group, the rest three
 PART1 = [(0, 0)]
-PART2 = [(0, 8), (1, 0), (1, 8)]
+PART2 = [(0, 1), (1, 0), (1, 1)]
 
 
 class Cfg:
     def __init__(self, D, bf16):
         assert D == 64
         self.D, self.bf16 = D, bf16
-        self.NB, self.NTQ, self.CPT = D // 32, D // 16, D // 32
-        self.NF = 4 * self.NB  # K^T fragments per tile (dQ A operands)
-        self.NKF = 2 * self.NTQ  # K / V row fragments per tile
-        self.exp_per_gap = 2
+        self.KS = D // 32  # 32-column steps of a row fragment
+        self.NDB = D // 16  # 16-row blocks of dQ^T
+        self.exp_per_gap = 1
+        self.min_cap = 12  # 16-cycle MFMAs: about half the 32x32x16 gap's issue room
         self.TBB = KT * D * 2
         self.OST = D + 4
-        self.mf = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
+        self.mf = "v_mfma_f32_16x16x32_bf16" if bf16 else "v_mfma_f32_16x16x32_f16"
         self.cvt = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
-        self.nvgpr, self.nagpr = 224, 224
-        self.SV = self.nvgpr  # 'stamps' timing builds: the stamp register (and one more)
+        self.nvgpr, self.nagpr = 192, 224
+        self.SV = self.nvgpr
         if "stamps" in asmgen.ABL:
             self.nvgpr += 2
 
     # AGPRs
-    def O(self, c, b):
-        return 16 * (2 * c + b)
+    def O(self, c, db, qb):
+        return 32 * c + 8 * db + 4 * qb
 
-    def Q(self, c, t):
-        return 64 + 4 * (4 * c + t)
+    def Q(self, c, qb, ks):
+        return 64 + 16 * c + 8 * qb + 4 * ks
 
-    def dO(self, c, t):
-        return 96 + 4 * (4 * c + t)
+    def dO(self, c, qb, ks):
+        return 96 + 16 * c + 8 * qb + 4 * ks
 
-    def Kt(self, i):
-        return 128 + 4 * i
+    def Kt(self, db, s):
+        return 128 + 4 * (2 * db + s)
 
-    def Kr(self, f):
-        return 160 + 4 * f
+    def Kr(self, kb, ks):
+        return 160 + 4 * (2 * kb + ks)
 
-    def Vr(self, f):
-        return 192 + 4 * f
+    def Vr(self, kb, ks):
+        return 192 + 4 * (2 * kb + ks)
 
     # VGPRs
-    def S(self, c, kb, i=0):
-        return 32 * c + 16 * kb + i
+    def S(self, c, qb, kb, i=0):
+        return 32 * c + 16 * qb + 4 * kb + i
 
-    def dP(self, c, kb, i=0):
-        return 64 + 32 * c + 16 * kb + i
+    def dP(self, c, qb, kb, i=0):
+        return 64 + 32 * c + 16 * qb + 4 * kb + i
 
-    def NL(self, c):
-        return 128 + 16 * c
+    def NL(self, c, qb):
+        return 128 + 4 * (2 * c + qb)
 
-    def ND(self, c):
-        return 160 + 16 * c
+    def ND(self, c, qb):
+        return 144 + 4 * (2 * c + qb)
 
     def stg(self, tensor, cc):
-        return 192 + 8 * (tensor * self.CPT + cc)
+        return 160 + 8 * (tensor * 2 + cc)
 
     def koff(self, slot):
         return slot * self.TBB
@@ -109,88 +123,82 @@ class Cfg:
 
     @property
     def lds_bytes(self):
-        # K, V slots + Q block + dO block; the dQ stage reuses the front after a barrier
         return max(4 * self.TBB + 2 * ROWS * self.D * 2, ROWS * self.OST * 4)
-
-    def ktr_addr(self, i):
-        b, kb, s = i // 4, (i // 2) % 2, i % 2
-        return b, (kb * 32 + 16 * s) * self.D * 2
 
 
 def mfma(cfg, dst, a, b, c, c_is_zero=False):
     rd = R(rng(a[0], a[1], 4), "A") + R(rng(b[0], b[1], 4), "B")
     if not c_is_zero:
-        rd += R(rng(c[0], c[1], 16), "C")
-    ctxt = "0" if c_is_zero else rtxt(c[0], c[1], 16)
-    return Ins(f"{cfg.mf} {rtxt(dst[0], dst[1], 16)}, {rtxt(a[0], a[1], 4)}, {rtxt(b[0], b[1], 4)}, {ctxt}", "mfma",
-               rd, rng(dst[0], dst[1], 16))
+        rd += R(rng(c[0], c[1], 4), "C")
+    ctxt = "0" if c_is_zero else rtxt(c[0], c[1], 4)
+    return Ins(f"{cfg.mf} {rtxt(dst[0], dst[1], 4)}, {rtxt(a[0], a[1], 4)}, {rtxt(b[0], b[1], 4)}, {ctxt}", "mfma",
+               rd, rng(dst[0], dst[1], 4))
 
 
 def row_reads(cfg, slot, tensor):
-    """the 8 row fragments (kb, t) of the K (tensor 0) or V (1) tile in `slot` -> AGPRs"""
+    """the 8 row fragments (kb, ks) of the K (tensor 0) or V (1) tile in `slot` -> AGPRs"""
     out = []
     base = cfg.koff(slot) if tensor == 0 else cfg.voff(slot)
-    for f in range(cfg.NKF):
-        kb, t = f // cfg.NTQ, f % cfg.NTQ
-        d = cfg.Kr(f) if tensor == 0 else cfg.Vr(f)
-        out.append(Ins(f"ds_read_b128 {rtxt('a', d, 4)}, %[ka{t}] offset:{base + kb * 32 * cfg.D * 2}", "dsr", [],
-                       rng("a", d, 4)))
+    for kb in range(4):
+        for ks in range(cfg.KS):
+            d = cfg.Kr(kb, ks) if tensor == 0 else cfg.Vr(kb, ks)
+            out.append(Ins(f"ds_read_b128 {rtxt('a', d, 4)}, %[ka{ks}] offset:{base + kb * 16 * cfg.D * 2}", "dsr",
+                           [], rng("a", d, 4)))
     return tagged("lds", out)
 
 
-def ktr_reads(cfg, i, slot, earliest=0):
-    b, off = cfg.ktr_addr(i)
-    off += cfg.koff(slot)
-    d = cfg.Kt(i)
+def ktr_reads(cfg, db, s, slot, earliest=0):
+    off = cfg.koff(slot) + s * 32 * cfg.D * 2
+    d = cfg.Kt(db, s)
     return tagged("lds", [
-        Ins(f"ds_read_b64_tr_b16 {rtxt('a', d, 2)}, %[kt{b}_0] offset:{off}", "dsr", [], rng("a", d, 2),
+        Ins(f"ds_read_b64_tr_b16 {rtxt('a', d, 2)}, %[kt{db}_0] offset:{off}", "dsr", [], rng("a", d, 2),
             earliest=earliest),
-        Ins(f"ds_read_b64_tr_b16 {rtxt('a', d + 2, 2)}, %[kt{b}_1] offset:{off}", "dsr", [], rng("a", d + 2, 2),
+        Ins(f"ds_read_b64_tr_b16 {rtxt('a', d + 2, 2)}, %[kt{db}_1] offset:{off}", "dsr", [], rng("a", d + 2, 2),
             earliest=earliest)])
 
 
-def sdp_mfmas(cfg, c, zero_seed=False):
-    """S^T[c] = K Q^T - LSE*log2e and dP^T[c] = V dO^T - Delta, kb = 0 first (dS part 1 needs it)"""
+def sdp_mfmas(cfg, c):
+    """S^T and dP^T tiles of chain c, group (qb, s) by group in PART1 + PART2 order (the first
+    part's dS needs its tiles first)"""
     out = []
-    for kb in range(2):
-        for which in range(2):
-            for t in range(cfg.NTQ):
-                f = kb * cfg.NTQ + t
-                if which == 0:
-                    dst, a, b, seed = cfg.S(c, kb), cfg.Kr(f), cfg.Q(c, t), cfg.NL(c)
-                else:
-                    dst, a, b, seed = cfg.dP(c, kb), cfg.Vr(f), cfg.dO(c, t), cfg.ND(c)
-                cc = ("v", seed) if t == 0 else ("v", dst)
-                out.append(mfma(cfg, ("v", dst), ("a", a), ("a", b), cc))
+    for qb, s in PART1 + PART2:
+        for kb in (2 * s, 2 * s + 1):
+            for which in range(2):
+                for ks in range(cfg.KS):
+                    if which == 0:
+                        dst, a, b, seed = cfg.S(c, qb, kb), cfg.Kr(kb, ks), cfg.Q(c, qb, ks), cfg.NL(c, qb)
+                    else:
+                        dst, a, b, seed = cfg.dP(c, qb, kb), cfg.Vr(kb, ks), cfg.dO(c, qb, ks), cfg.ND(c, qb)
+                    cc = ("v", seed) if ks == 0 else ("v", dst)
+                    out.append(mfma(cfg, ("v", dst), ("a", a), ("a", b), cc))
     return out
 
 
 def dq_mfmas(cfg, c, first=False):
-    """dQ^T[c][b] += K^T dS^T[c]: b-major, so K^T slot i is free after MFMA i"""
+    """dQ^T[c][db][qb] += K^T[db][s] dS^T[c][qb][s]"""
     out = []
-    for b in range(cfg.NB):
-        for kb in range(2):
-            for s in range(2):
-                i = b * 4 + kb * 2 + s
-                z = first and kb == 0 and s == 0
-                out.append(mfma(cfg, ("a", cfg.O(c, b)), ("a", cfg.Kt(i)), ("v", cfg.S(c, kb, 8 * s)),
-                                ("a", cfg.O(c, b)), c_is_zero=z))
+    for db in range(cfg.NDB):
+        for s in range(2):
+            for qb in range(2):
+                z = first and s == 0
+                out.append(mfma(cfg, ("a", cfg.O(c, db, qb)), ("a", cfg.Kt(db, s)), ("v", cfg.S(c, qb, 2 * s)),
+                                ("a", cfg.O(c, db, qb)), c_is_zero=z))
     return out
 
 
 def ds_part(cfg, c, groups):
-    """dS of the given 8-score groups (kb, first score) of chain c: exp2, * dP', packed in place
-    (per group: exps and products first, then the 4 packs)"""
+    """dS of the given groups (qb, s) of chain c: exp2, * dP', packed in place"""
     out = []
-    for kb, g0 in groups:
-        for i in range(g0, g0 + 8):
-            s = cfg.S(c, kb, i)
-            out.append(valu(f"v_exp_f32 v{s}, v{s}", [f"v{s}"], [f"v{s}"], kind="exp"))
-        for i in range(g0, g0 + 8):
-            s, d = cfg.S(c, kb, i), cfg.dP(c, kb, i)
-            out.append(valu(f"v_mul_f32 v{s}, v{s}, v{d}", [f"v{s}", f"v{d}"], [f"v{s}"]))
+    for qb, s in groups:
+        base, dbase = cfg.S(c, qb, 2 * s), cfg.dP(c, qb, 2 * s)
+        for i in range(8):
+            r = base + i
+            out.append(valu(f"v_exp_f32 v{r}, v{r}", [f"v{r}"], [f"v{r}"], kind="exp"))
+        for i in range(8):
+            r, d = base + i, dbase + i
+            out.append(valu(f"v_mul_f32 v{r}, v{r}, v{d}", [f"v{r}", f"v{d}"], [f"v{r}"]))
         for ii in range(4):
-            d, a, b = cfg.S(c, kb, g0 + ii), cfg.S(c, kb, g0 + 2 * ii), cfg.S(c, kb, g0 + 2 * ii + 1)
+            d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
             out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
     return tagged("sm", out)
 
@@ -198,7 +206,7 @@ def ds_part(cfg, c, groups):
 def staging_loads(cfg, tensor):
     rs = "%[rsk]" if tensor == 0 else "%[rsv]"
     out = []
-    for cc in range(cfg.CPT):
+    for cc in range(2):
         base = cfg.stg(tensor, cc)
         for h in range(2):
             off = f" offset:{16 * h}" if h else ""
@@ -216,7 +224,7 @@ def staging_convert(cfg, tensor, slot):
     out = []
     toff = cfg.koff(slot) if tensor == 0 else cfg.voff(slot)
     rows_per_chunk_step = 256 // (cfg.D // 8)
-    for cc in range(cfg.CPT):
+    for cc in range(2):
         base = cfg.stg(tensor, cc)
         for ii in range(4):
             d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
@@ -226,22 +234,27 @@ def staging_convert(cfg, tensor, slot):
     return tagged("stg", out)
 
 
+def kt_all(cfg, slot):
+    out = []
+    for db in range(cfg.NDB):
+        for s in range(2):
+            out += ktr_reads(cfg, db, s, slot)
+    return out
+
+
 def body(cfg, p, log):
     q = 1 - p
     seq = []
     conv = staging_convert(cfg, 0, q)
     for ins in conv:
-        ins.earliest = 4
+        ins.earliest = 8
     seq += stamp(cfg.SV)
     seq += schedule_phase(cfg, sdp_mfmas(cfg, 0), [ds_part(cfg, 1, PART2), conv], f"P1.{p}", log)
     seq += stamp(cfg.SV)
     seq += schedule_phase(cfg, dq_mfmas(cfg, 1), [ds_part(cfg, 0, PART1), staging_convert(cfg, 1, q),
                                                   staging_loads(cfg, 0)], f"P2.{p}", log)
     seq += stamp(cfg.SV)
-    kt = []
-    for i in range(cfg.NF):
-        kt += ktr_reads(cfg, i, p)
-    seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [ds_part(cfg, 0, PART2), kt], f"P3.{p}", log)
+    seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [ds_part(cfg, 0, PART2), kt_all(cfg, p)], f"P3.{p}", log)
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     seq += stamp(cfg.SV)
     seq.append(tagged("bar", [Ins("s_barrier", "bar")])[0])
@@ -252,34 +265,37 @@ def body(cfg, p, log):
 
 
 def prologue(cfg):
-    D, NTQ = cfg.D, cfg.NTQ
+    D = cfg.D
     seq = [Ins("s_mov_b32 s98, 0", "salu", [], ["s98"])] if "stamps" in asmgen.ABL else []
     seq += stamp(cfg.SV)
     seq += staging_loads(cfg, 0) + staging_loads(cfg, 1) + [goff_inc(cfg)]
-    # Q and dO fragments of both chains (blocks in LDS at %[qb] / %[db] + this wave's rows)
-    for t in range(NTQ):
-        seq.append(valu(f"v_add_u32 v{t}, %[qb], %[ka{t}]", [], [f"v{t}"]))
-        seq.append(valu(f"v_add_u32 v{4 + t}, %[db], %[ka{t}]", [], [f"v{4 + t}"]))
+    # Q and dO fragments of the wave's 4 query blocks (blocks in LDS at %[qb] / %[db])
+    for ks in range(cfg.KS):
+        seq.append(valu(f"v_add_u32 v{ks}, %[qb], %[ka{ks}]", [], [f"v{ks}"]))
+        seq.append(valu(f"v_add_u32 v{2 + ks}, %[db], %[ka{ks}]", [], [f"v{2 + ks}"]))
     for c in range(2):
-        for t in range(NTQ):
-            seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.Q(c, t), 4)}, v{t} offset:{c * 32 * D * 2}", "dsr",
-                           R([f"v{t}"]), rng("a", cfg.Q(c, t), 4)))
-            seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.dO(c, t), 4)}, v{4 + t} offset:{c * 32 * D * 2}", "dsr",
-                           R([f"v{4 + t}"]), rng("a", cfg.dO(c, t), 4)))
+        for qb in range(2):
+            for ks in range(cfg.KS):
+                off = (32 * c + 16 * qb) * D * 2
+                seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.Q(c, qb, ks), 4)}, v{ks} offset:{off}", "dsr",
+                               R([f"v{ks}"]), rng("a", cfg.Q(c, qb, ks), 4)))
+                seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.dO(c, qb, ks), 4)}, v{2 + ks} offset:{off}", "dsr",
+                               R([f"v{2 + ks}"]), rng("a", cfg.dO(c, qb, ks), 4)))
     seq += row_reads(cfg, 0, 0) + row_reads(cfg, 0, 1)
-    # the lane-constant seeds: -LSE*log2e and -Delta of this lane's row in each chain
+    # the seeds: -LSE*log2e and -Delta of the lane's query row in each 16-row block
     for c in range(2):
-        for i in range(16):
-            seq.append(valu(f"v_mov_b32 v{cfg.NL(c) + i}, %[nl{c}]", [], [f"v{cfg.NL(c) + i}"]))
-            seq.append(valu(f"v_mov_b32 v{cfg.ND(c) + i}, %[nd{c}]", [], [f"v{cfg.ND(c) + i}"]))
+        for qb in range(2):
+            for i in range(4):
+                seq.append(valu(f"v_mov_b32 v{cfg.NL(c, qb) + i}, %[nl{2 * c + qb}]", [], [f"v{cfg.NL(c, qb) + i}"]))
+                seq.append(valu(f"v_mov_b32 v{cfg.ND(c, qb) + i}, %[nd{2 * c + qb}]", [], [f"v{cfg.ND(c, qb) + i}"]))
     seq += sdp_mfmas(cfg, 0) + sdp_mfmas(cfg, 1)
     seq += ds_part(cfg, 0, PART1) + ds_part(cfg, 0, PART2) + ds_part(cfg, 1, PART1)
-    for i in range(cfg.NF):
-        seq += ktr_reads(cfg, i, 0)
-    for b in range(cfg.NB):
-        for i in range(16):
-            r = cfg.O(1, b) + i
-            seq.append(valu(f"v_accvgpr_write_b32 a{r}, 0", [], [f"a{r}"]))
+    seq += kt_all(cfg, 0)
+    for db in range(cfg.NDB):
+        for qb in range(2):
+            for i in range(4):
+                r = cfg.O(1, db, qb) + i
+                seq.append(valu(f"v_accvgpr_write_b32 a{r}, 0", [], [f"a{r}"]))
     seq += dq_mfmas(cfg, 0, first=True)
     seq += staging_convert(cfg, 0, 1) + staging_convert(cfg, 1, 1)
     seq += staging_loads(cfg, 0) + staging_loads(cfg, 1) + [goff_inc(cfg)]
@@ -295,14 +311,16 @@ def epilogue(cfg):
     seq += ds_part(cfg, 1, PART2)
     seq += dq_mfmas(cfg, 1)
     seq.append(Ins("s_barrier", "bar"))
+    # dQ^T[c][db][qb] reg i: d = 16 db + 4g + i, query 32c + 16qb + (l & 15) -> stage row, 4 columns
     for c in range(2):
-        for b in range(cfg.NB):
-            for g in range(4):
-                r = cfg.O(c, b) + 4 * g
-                off = (c * 32 * cfg.OST + 32 * b + 8 * g) * 4
+        for db in range(cfg.NDB):
+            for qb in range(2):
+                r = cfg.O(c, db, qb)
+                off = ((32 * c + 16 * qb) * cfg.OST + 16 * db) * 4
                 seq.append(Ins(f"ds_write_b128 %[oa], {rtxt('a', r, 4)} offset:{off}", "dsw", R(rng("a", r, 4)), []))
     if "stamps" in asmgen.ABL:
-        # the stamps into stage columns 2 / 6, the count into 3 / 7 (gen_fwd_hs.py's layout)
+        # the stamps through %[sa], the 32x32 build's stage address (row l & 31, column
+        # 4 (l >> 5) + 2), so tools/stamps_hs.py decodes both builds alike
         seq += stamp(cfg.SV)
         sv, sc = cfg.SV, cfg.SV + 1
         seq += [Ins("s_nop 4", "nop"),
@@ -311,8 +329,8 @@ def epilogue(cfg):
                 valu(f"v_mov_b32 v{sc}, s98", [], [f"v{sc}"]),
                 valu(f"v_cvt_f32_u32 v{sc}, v{sc}", [f"v{sc}"], [f"v{sc}"]),
                 Ins("s_nop 4", "nop"),
-                Ins(f"ds_write_b32 %[oa], v{sv} offset:8", "dsw", R([f"v{sv}"]), []),
-                Ins(f"ds_write_b32 %[oa], v{sc} offset:12", "dsw", R([f"v{sc}"]), [])]
+                Ins(f"ds_write_b32 %[sa], v{sv} offset:8", "dsw", R([f"v{sv}"]), []),
+                Ins(f"ds_write_b32 %[sa], v{sc} offset:12", "dsw", R([f"v{sc}"]), [])]
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     return seq
 
@@ -351,11 +369,14 @@ def build(cfg):
 
 def operands(cfg):
     outs = ['[cnt] "+s"(hs_cnt)', '[goff] "+s"(hs_goff)']
-    ins = [f'[ka{t}] "v"(hs_ka[{t}])' for t in range(cfg.NTQ)]
-    ins += [f'[kt{b}_{k}] "v"(hs_kt[{b}][{k}])' for b in range(cfg.NB) for k in range(2)]
-    ins += [f'[vo{c}] "v"(hs_vo[{c}])' for c in range(cfg.CPT)]
-    ins += ['[lo] "v"(hs_lo)', '[oa] "v"(hs_oa)', '[nl0] "v"(hs_nl0)', '[nl1] "v"(hs_nl1)', '[nd0] "v"(hs_nd0)',
-            '[nd1] "v"(hs_nd1)', '[rsk] "s"(hs_rsk)', '[rsv] "s"(hs_rsv)', '[qb] "s"(hs_qb)', '[db] "s"(hs_db)']
+    ins = [f'[ka{ks}] "v"(hs_ka[{ks}])' for ks in range(cfg.KS)]
+    ins += [f'[kt{db}_{k}] "v"(hs_kt[{db}][{k}])' for db in range(cfg.NDB) for k in range(2)]
+    ins += [f'[vo{c}] "v"(hs_vo[{c}])' for c in range(2)]
+    ins += [f'[nl{i}] "v"(hs_nl[{i}])' for i in range(4)] + [f'[nd{i}] "v"(hs_nd[{i}])' for i in range(4)]
+    ins += ['[lo] "v"(hs_lo)', '[oa] "v"(hs_oa)', '[rsk] "s"(hs_rsk)', '[rsv] "s"(hs_rsv)', '[qb] "s"(hs_qb)',
+            '[db] "s"(hs_db)']
+    if "stamps" in asmgen.ABL:
+        ins.append('[sa] "v"(hs_sa)')
     clob = [f'"v{i}"' for i in range(cfg.nvgpr)] + [f'"a{i}"' for i in range(cfg.nagpr)] + ['"vcc"', '"scc"', '"memory"']
     if "stamps" in asmgen.ABL:
         clob += asmgen.STAMP_CLOBBERS

@@ -1195,7 +1195,8 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
 // Hand-scheduled dQ (D = 64; S % 64 == 0, S >= 128), r05.
 // ---------------------------------------------------------------------------
 // One workgroup = 4 waves = 256 query rows, one wave per SIMD; each wave keeps 64 query
-// rows as two 32-row chains (Q, dO fragments and dQᵀ accumulators in AGPRs) and streams
+// rows as two 32-row chains of two 16-row blocks on the lane (Q, dO fragments and dQᵀ
+// accumulators in AGPRs; every product on v_mfma_f32_16x16x32) and streams
 // the head's 64-key K/V tiles through LDS.  Per tile four MFMA phases alternate the
 // chains: Sᵀ and dPᵀ of one chain while the other chain's dS is formed in the MFMA gaps,
 // then that chain's dQᵀ += Kᵀ dSᵀ.  The tile loop is the generated inline-asm block of
@@ -1209,15 +1210,9 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
 #define FA2_DQ_INC "fa2_bwd_dq_hs.inc"  // (timing-only ablation builds name another, tools/r05_hs_abl.sh)
 #endif
 #include FA2_DQ_INC
-#ifndef FA2_DQ16_INC
-#define FA2_DQ16_INC "fa2_bwd_dq16_hs.inc"
-#endif
-#include FA2_DQ16_INC
 namespace fa2f16b {
 
-// M16: the loop on v_mfma_f32_16x16x32 (fa2_bwd_dq16_hs.inc, gen/gen_bwd_dq16.py): 16-row
-// query blocks on the lane, seeds per 16-row block, dQᵀ tiles of 16 d x 16 queries
-template <int D, bool M16>
+template <int D>
 __global__ void __launch_bounds__(256, 1)
 fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                      const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
@@ -1269,68 +1264,43 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
     vs.store(smem + 2 * TB, 1.f, tid);
     __syncthreads();
 
-    // per-lane LDS byte offsets of the row and transposed fragment reads (the 32x32x16 or
-    // the 16x16x32 operand maps)
-    constexpr int NKA = M16 ? D / 32 : D / 16, NKT = M16 ? D / 16 : D / 32;
-    int hs_ka[NKA], hs_kt[NKT][2], hs_vo[D / 32];
-    if constexpr (M16) {
-        FragOffsets16<D> fo;
-        fo.init(lane);
+    // per-lane LDS byte offsets of the row and transposed fragment reads (16x16x32 maps)
+    FragOffsets16<D> fo;
+    fo.init(lane);
+    int hs_ka[D / 32], hs_kt[D / 16][2], hs_vo[D / 32];
 #pragma unroll
-        for (int t = 0; t < NKA; ++t) hs_ka[t] = fo.row[t] * 2;
+    for (int t = 0; t < D / 32; ++t) hs_ka[t] = fo.row[t] * 2;
 #pragma unroll
-        for (int b = 0; b < NKT; ++b) {
-            hs_kt[b][0] = fo.tr[b][0] * 2;
-            hs_kt[b][1] = fo.tr[b][1] * 2;
-        }
-    } else {
-        FragOffsets<D> fo;
-        fo.init(lane);
-#pragma unroll
-        for (int t = 0; t < NKA; ++t) hs_ka[t] = fo.row[t] * 2;
-#pragma unroll
-        for (int b = 0; b < NKT; ++b) {
-            hs_kt[b][0] = fo.tr[b][0] * 2;
-            hs_kt[b][1] = fo.tr[b][1] * 2;
-        }
+    for (int b = 0; b < D / 16; ++b) {
+        hs_kt[b][0] = fo.tr[b][0] * 2;
+        hs_kt[b][1] = fo.tr[b][1] * 2;
     }
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) hs_vo[c] = ks.voff[c];
     const int hs_lo = ks.loff[0] * 2;
-    // the dQ stage address (16x16: row l & 15 of each 16-row block, columns 4 (l >> 4) ..)
-    // and the lane-constant seeds -LSE·log2e, -Δ of the lane's row in each 32-row chain
-    // (16x16: each 16-row block)
+    // the dQ stage address (row l & 15 of each 16-row block, columns 4 (l >> 4) ..) and the
+    // lane-constant seeds -LSE·log2e, -Δ of the lane's row in each 16-row block
     const int g16 = lane >> 4, i16 = lane & 15;
-    const int hs_sa = ((wave * 64 + r) * OST + 4 * h) * 4;  // (the 32x32 stage address; 'stamps' builds)
-    const int hs_oa = M16 ? ((wave * 64 + i16) * OST + 4 * g16) * 4 : hs_sa;
+    const int hs_sa = ((wave * 64 + r) * OST + 4 * h) * 4;  // (row l & 31, columns 4 (l >> 5): 'stamps' builds)
+    const int hs_oa = ((wave * 64 + i16) * OST + 4 * g16) * 4;
     (void)hs_sa;
-    constexpr int NSEED = M16 ? 4 : 2;
-    float hs_nl[NSEED], hs_nd[NSEED];
+    float hs_nl[4], hs_nd[4];
 #pragma unroll
-    for (int c = 0; c < NSEED; ++c) {
-        const int row = wave * 64 + (M16 ? 16 * c + i16 : 32 * c + r);
+    for (int c = 0; c < 4; ++c) {
+        const int row = wave * 64 + 16 * c + i16;
         hs_nl[c] = rowc[0][row];
         hs_nd[c] = -rowc[1][row];
     }
-    const float hs_nl0 = hs_nl[0], hs_nl1 = hs_nl[1], hs_nd0 = hs_nd[0], hs_nd1 = hs_nd[1];
     const __amdgpu_buffer_rsrc_t hs_rsk = ks.rs, hs_rsv = vs.rs;
     const int hs_qb = __builtin_amdgcn_readfirstlane(4 * TB * 2 + wave * 64 * D * 2);
     const int hs_db = __builtin_amdgcn_readfirstlane(8 * TB * 2 + wave * 64 * D * 2);
     int hs_cnt = __builtin_amdgcn_readfirstlane(S / KT - 1);
     int hs_goff = __builtin_amdgcn_readfirstlane(KT * D * 4);
-    if constexpr (M16) {
 #ifdef FA2_TILE_BF16
-        asm volatile(FA2_DQ16_ASM_D64_BF16 : FA2_DQ16_OUTPUTS_D64 : FA2_DQ16_INPUTS_D64 : FA2_DQ16_CLOBBERS_D64);
+    asm volatile(FA2_DQ_ASM_D64_BF16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
 #else
-        asm volatile(FA2_DQ16_ASM_D64_F16 : FA2_DQ16_OUTPUTS_D64 : FA2_DQ16_INPUTS_D64 : FA2_DQ16_CLOBBERS_D64);
+    asm volatile(FA2_DQ_ASM_D64_F16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
 #endif
-    } else {
-#ifdef FA2_TILE_BF16
-        asm volatile(FA2_DQ_ASM_D64_BF16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
-#else
-        asm volatile(FA2_DQ_ASM_D64_F16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
-#endif
-    }
     // dQ rows [wave*64 + c*32 + q][OST] (unscaled) -> HBM as whole rows, times 1/sqrt(D)
     constexpr int LPR = D / 4, RPI = 64 / LPR;
     const float dscale = 1.f / __builtin_sqrtf((float)D);
@@ -1811,23 +1781,16 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     int ksp = tune_knob("DQ_KS", 0);
     if constexpr (D == 64) {
         // hand-scheduled kernel (r05): whole 64-key tiles, and a grid of at least one
-        // 256-row workgroup per CU.  DQ_HS (tests and tools): 2 forces it, 1 forces its
-        // 32x32x16 form (A/B; an error where they cannot serve), 0 disables it
+        // 256-row workgroup per CU.  DQ_HS (tests and tools): 1 forces it (an error where it
+        // cannot serve), 0 disables it
         const int hs = tune_knob("DQ_HS", -1);
         const bool fits = S % 64 == 0 && S >= 128;
-        if (hs >= 1 && !fits) return hipErrorInvalidValue;
+        if (hs == 1 && !fits) return hipErrorInvalidValue;
         const long hgrid = (long)bh * ((S + 255) / 256);
-        if (fits && (hs >= 1 || (hs < 0 && nw == 0 && ksp == 0 && hgrid >= cu_count()))) {
+        if (fits && (hs == 1 || (hs < 0 && nw == 0 && ksp == 0 && hgrid >= cu_count()))) {
             if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
-            // the 16x16x32 loop by default: r05 in-process A/B against the 32x32x16 loop
-            // (DQ_HS = 1): C3 112.7 vs 118.8 us, B2_H8_S4096 99.9 vs 106.0, B16_H16_S2048
-            // 440.5 vs 451.5 (profiles/r05/dq16/)
-            if (hs != 1)
-                hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D, true>), dim3((unsigned)hgrid), dim3(256), 0, stream,
-                                   q, k, v, dout, lse, delta, dq, S, o);
-            else
-                hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D, false>), dim3((unsigned)hgrid), dim3(256), 0,
-                                   stream, q, k, v, dout, lse, delta, dq, S, o);
+            hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D>), dim3((unsigned)hgrid), dim3(256), 0, stream, q, k, v,
+                               dout, lse, delta, dq, S, o);
             return hipGetLastError();
         }
     }

@@ -56,12 +56,11 @@ def _case(shape, seed=3, gauss=False):
     return (q, k, v, do, eo.astype(np.float32), el.astype(np.float32)), (edq, edk, edv, edl)
 
 
-HS_KNOBS = [{"DQ_HS": 1, "DKDV_HS": 0}, {"DQ_HS": 0, "DKDV_HS": 1}, {"DQ_HS": 1, "DKDV_HS": 1},
-            {"DQ_HS": 2, "DKDV_HS": 0}]
+HS_KNOBS = [{"DQ_HS": 1, "DKDV_HS": 0}, {"DQ_HS": 0, "DKDV_HS": 1}, {"DQ_HS": 1, "DKDV_HS": 1}]
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-@pytest.mark.parametrize("knobs", HS_KNOBS, ids=["dq_hs", "dkdv_hs", "both_hs", "dq16_hs"])
+@pytest.mark.parametrize("knobs", HS_KNOBS, ids=["dq_hs", "dkdv_hs", "both_hs"])
 @pytest.mark.parametrize("shape", DQ_SHAPES + [(1, 1, 384, 64), (1, 1, 448, 64)], ids=lambda s: "B%d_H%d_S%d_D%d" % s)
 def test_hs_full_backward(shape, knobs, precision):
     """fa2_backward's two-kernel plan with the hand-scheduled dQ (Δ fused, written out for
@@ -79,13 +78,11 @@ def test_hs_full_backward(shape, knobs, precision):
         assert maxerr(g, exp) < TOL[precision] * max(1.0, float(np.abs(exp).max()))
 
 
-@pytest.mark.parametrize("form", [1, 2], ids=["m32", "m16"])
 @pytest.mark.parametrize("fused_delta", [True, False], ids=["delta_fused", "delta_given"])
 @pytest.mark.parametrize("shape", [(1, 2, 320, 64), (2, 2, 1024, 64)], ids=lambda s: "B%d_H%d_S%d_D%d" % s)
-def test_hs_dq_entry_points(shape, fused_delta, form):
-    """fa2_backward_dq_delta (Δ from the staged O rows, written out) and fa2_backward_dq (Δ
-    read), both loop forms (DQ_HS = 1: 32x32x16, 2: 16x16x32)"""
-    fa2amd.tune_set("DQ_HS", form)
+def test_hs_dq_entry_points(shape, fused_delta):
+    """fa2_backward_dq_delta (Δ from the staged O rows, written out) and fa2_backward_dq (Δ read)"""
+    fa2amd.tune_set("DQ_HS", 1)
     (q, k, v, do, o, lse), (edq, _, _, edl) = _case(shape, seed=7, gauss=True)
     tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
     dq = torch.empty_like(tq)
@@ -134,17 +131,15 @@ def test_hs_dkdv_deterministic_and_default():
     assert maxerr(res[1][1][:1, :2], edv) < TOL["fp16"] * max(1.0, float(np.abs(edv).max()))
 
 
-@pytest.mark.parametrize("form", [1, 2], ids=["m32", "m16"])
-def test_hs_dq_deterministic_and_default(form):
-    """bitwise repeatable; at C3's grid the default dQ launch is the hand-scheduled one
-    (DQ_HS = -1 runs the same kernel as DQ_HS = 2, the 16x16x32 loop)"""
+def test_hs_dq_deterministic_and_default():
+    """bitwise repeatable; at C3's grid the default dQ launch is the hand-scheduled one"""
     B, H, S, D = 4, 16, 2048, 64
     q, k, v = fo.harness_inputs(B, H, S, D, seed=2)
     do = np.random.RandomState(9).randn(B, H, S, D).astype(np.float32)
     tq, tk, tv, tdo = cuda(q, k, v, do)
     o, lse = fa2amd.forward(tq, tk, tv, "fp16")
     res = []
-    for hs in ((1, 1, 1, 0) if form == 1 else (-1, 2, 2, 0)):
+    for hs in (-1, 1, 1, 0):
         fa2amd.tune_set("DQ_HS", hs)
         dq, dk, dv = fa2amd.backward(tq, tk, tv, o, tdo, lse, "fp16")
         torch.cuda.synchronize()

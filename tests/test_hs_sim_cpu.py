@@ -36,15 +36,10 @@ def test_forward_loop_flags_a_late_spike(D):
     assert "restart flag True" in sim("--kernel", "fwd", "--D", str(D), "--S", "256", "--spike")
 
 
-@pytest.mark.parametrize("S,block", [(128, 0), (192, 0), (256, 0), (512, 1)])
-def test_dq_loop(S, block):
-    sim("--kernel", "dq", "--D", "64", "--S", str(S), "--block", str(block))
-
-
-@pytest.mark.parametrize("S,block,bf16", [(128, 0, False), (256, 0, True), (320, 0, False), (512, 1, False)])
-def test_dq16_loop(S, block, bf16):
-    """the 16x16x32 form of the dQ loop"""
-    sim("--kernel", "dq16", "--D", "64", "--S", str(S), "--block", str(block), *(["--bf16"] if bf16 else []))
+@pytest.mark.parametrize("S,block,bf16", [(128, 0, False), (192, 0, False), (256, 0, True), (320, 0, False),
+                                          (512, 1, False)])
+def test_dq_loop(S, block, bf16):
+    sim("--kernel", "dq", "--D", "64", "--S", str(S), "--block", str(block), *(["--bf16"] if bf16 else []))
 
 
 @pytest.mark.parametrize("S,block,bf16", [(192, 0, False), (256, 0, False), (320, 0, True), (384, 0, False),
@@ -53,7 +48,7 @@ def test_dkdv_loop(S, block, bf16):
     sim("--kernel", "dkdv", "--D", "64", "--S", str(S), "--block", str(block), *(["--bf16"] if bf16 else []))
 
 
-@pytest.mark.parametrize("gen", ["gen_fwd_hs.py", "gen_bwd_dq.py", "gen_bwd_dq16.py", "gen_bwd_dkdv.py"])
+@pytest.mark.parametrize("gen", ["gen_fwd_hs.py", "gen_bwd_dq.py", "gen_bwd_dkdv.py"])
 def test_generated_loops_are_current(gen):
     """each committed kernels/*.inc is what its generator writes from its current source"""
     r = subprocess.run([sys.executable, os.path.join(GEN, gen), "--check"], capture_output=True, text=True,

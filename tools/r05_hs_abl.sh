@@ -1,6 +1,6 @@
 #!/bin/bash
 # r05: timing-only ablation builds of the hand-scheduled loops (results invalid):
-#   tools/r05_hs_abl.sh name:kernel:abl1,abl2 ...   (kernel: fwd | fwd16 | dq | dq16 | dkdv)
+#   tools/r05_hs_abl.sh name:kernel:abl1,abl2 ...   (kernel: fwd | dq | dkdv)
 #   -> cuda-flash-attention_amd/abl/<name>/libfa2amd.so
 # Only the kernel's translation units are recompiled (the product objects are copied).
 set -e
@@ -15,7 +15,6 @@ for spec in "$@"; do
     fwd)  G=gen_fwd_hs.py;   M=FA2_HS_INC; rm -f "$D"/build/kernel_fa2_optimized_f16.o "$D"/build/kernel_fa2_optimized_bf16.o ;;
     dq)   G=gen_bwd_dq.py;   M=FA2_DQ_INC; rm -f "$D"/build/f-attn2-backward_f16.o "$D"/build/f-attn2-backward_bf16.o ;;
     dkdv) G=gen_bwd_dkdv.py; M=FA2_DK_INC; rm -f "$D"/build/f-attn2-backward_f16.o "$D"/build/f-attn2-backward_bf16.o ;;
-    dq16) G=gen_bwd_dq16.py; M=FA2_DQ16_INC; rm -f "$D"/build/f-attn2-backward_f16.o "$D"/build/f-attn2-backward_bf16.o ;;
   esac
   python3 "$P/gen/$G" --abl "$A" --out "$D/abl.inc" > /dev/null
   make -s -j8 -C "$P" lib BUILD="$D/build" LIBDIR="$D" EXTRA="-D$M=\\\"$D/abl.inc\\\""

@@ -7,7 +7,5 @@ A=cuda-flash-attention_amd/abl
 timeout -k 10 120 python tools/stamps_hs.py --lib $A/fw_stamps/libfa2amd.so \
   --shape 4,16,2048,64 --shape 1,1,2048,64 --shape 1,16,2048,64 --shape 8,16,4096,128 > $OUT/fwd.log 2>&1 &&
 timeout -k 10 120 python tools/stamps_hs.py --kernel dq --lib $A/dq_stamps/libfa2amd.so \
-  --shape 4,16,2048,64 --shape 1,1,2048,64 > $OUT/dq.log 2>&1 &&
-timeout -k 10 120 python tools/stamps_hs.py --kernel dq16 --lib $A/dq16_stamps/libfa2amd.so \
-  --shape 4,16,2048,64 --shape 1,1,2048,64 > $OUT/dq16.log 2>&1 || exit $?
+  --shape 4,16,2048,64 --shape 1,1,2048,64 > $OUT/dq.log 2>&1 || exit $?
 echo done > $OUT/status.txt

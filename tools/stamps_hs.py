@@ -22,14 +22,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", required=True)
     ap.add_argument("--shape", action="append", default=[])
-    ap.add_argument("--kernel", choices=["fwd", "dq", "dq16"], default="fwd")
+    ap.add_argument("--kernel", choices=["fwd", "dq"], default="fwd")
     a = ap.parse_args()
     import torch
     import fa2amd
 
     fa2amd.use_library(os.path.join(ROOT, a.lib) if not os.path.isabs(a.lib) else a.lib)
     fa2amd.tune_set("FWD_HS", 1)
-    fa2amd.tune_set("DQ_HS", 2 if a.kernel == "dq16" else 1)
+    fa2amd.tune_set("DQ_HS", 1)
     names = ["P1 (QK A | sm B)", "P2 (PV B | sm A)", "P3 (QK B | sm A) + drain", "barrier wait", "P4 (PV A | sm B)"]
     if a.kernel != "fwd":
         names = ["P1 (SdP A | dS B)", "P2 (dQ B | dS A)", "P3 (SdP B | dS A) + drain", "barrier wait",
