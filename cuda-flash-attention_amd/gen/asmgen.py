@@ -236,11 +236,12 @@ def fix_hazards(block, preds):
 
 
 ABL = set()  # timing-only ablations (--abl a,b --out file): results are invalid, never the product .inc
+EXACT_ABL = {"nopk", "addrr"}  # variants that keep the product's results (and its flag)
 
 
 def ablate(seq):
     """drop the loop-body instructions the active ablations name"""
-    if not ABL:
+    if not ABL - EXACT_ABL:
         return seq
     out = []
     for i in seq:
