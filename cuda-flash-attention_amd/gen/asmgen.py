@@ -63,6 +63,15 @@ def valu(text, rd, wr, kind="valu"):
     return Ins(text, kind, R(rd), wr)
 
 
+def thirds(seq):
+    """seq in three consecutive chunks of near-equal length (staging loads spread over three
+    phases: bunched into one 8-MFMA phase they ask for ~64 B/clk per CU, the texture unit's
+    whole rate, and the issuing waves wait; the 'nospread' build keeps the old placement)"""
+    n = len(seq)
+    a, b = -(-n // 3), -(-2 * n // 3)
+    return seq[:a], seq[a:b], seq[b:]
+
+
 def schedule_phase(cfg, mfmas, streams, name, log):
     """cfg: any object with exp_per_gap"""
     nM = len(mfmas)
@@ -236,7 +245,7 @@ def fix_hazards(block, preds):
 
 
 ABL = set()  # timing-only ablations (--abl a,b --out file): results are invalid, never the product .inc
-EXACT_ABL = {"nopk", "addrr"}  # variants that keep the product's results (and its flag)
+EXACT_ABL = {"addrr", "nospread"}  # variants that keep the product's results (and its flag)
 
 
 def ablate(seq):

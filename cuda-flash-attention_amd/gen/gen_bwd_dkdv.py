@@ -43,7 +43,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import asmgen  # noqa: E402
-from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, insert_waits_multi, rng, rtxt, schedule_phase, tagged, valu  # noqa: E402,E501
+from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, insert_waits_multi, rng, rtxt, schedule_phase, tagged, thirds, valu  # noqa: E402,E501
 
 QT = 64  # queries per step
 KEYS = 256  # keys per workgroup
@@ -265,18 +265,26 @@ def body(cfg, j3, log):
     # P2: dV, dK of B (j-1) | P, dS of A key block 0; seeds of B for P3 (A's done with the ring);
     #     loads of step j+2
     sd = seed_reads(cfg, s, 0, 1, 0) + seed_reads(cfg, s, 1, 1, 1)
-    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 1), [pds_part(cfg, 0, 0), sd, staging_loads(cfg)], f"P2.{j3}", log)
+    # loads of step j+2 (staging registers free since P1's convert) spread over P2, P3, P4;
+    # the offset adds after the last of them
+    stl = staging_loads(cfg)
+    if "nospread" in asmgen.ABL:
+        ld = (stl, [], [])
+    else:
+        ld = thirds(stl[:-2])
+        ld = (ld[0], ld[1], ld[2] + stl[-2:])
+    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 1), [pds_part(cfg, 0, 0), sd, list(ld[0])], f"P2.{j3}", log)
     # P3: S, dP of B | P, dS of A key block 1; A's trop frags for P4 (the ring is free after P2)
     pre = []
     for k in range(8):
         pre += trop_reads(cfg, s, 0, k)
-    seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [pds_part(cfg, 0, 1), pre], f"P3.{j3}", log)
+    seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [pds_part(cfg, 0, 1), pre, list(ld[1])], f"P3.{j3}", log)
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     seq.append(tagged("bar", [Ins("s_barrier", "bar")])[0])
     # P4: dV, dK of A | P, dS of B key block 0; Q/dO rows and A's seeds of step j+1 (the seed
     #     ring is free after P3)
     nxt = rowop_reads(cfg, n) + seed_reads(cfg, n, 0, 0, 0, earliest=2) + seed_reads(cfg, n, 1, 0, 1, earliest=2)
-    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 0), [pds_part(cfg, 1, 0), nxt], f"P4.{j3}", log)
+    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 0), [pds_part(cfg, 1, 0), nxt, list(ld[2])], f"P4.{j3}", log)
     return seq
 
 

@@ -53,7 +53,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import asmgen  # noqa: E402
-from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, stamp, tagged, valu  # noqa: E402,E501
+from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, stamp, tagged, thirds, valu  # noqa: E402,E501
 
 KT = 64
 ROWS = 256
@@ -251,16 +251,22 @@ def body(cfg, p, log):
     seq += stamp(cfg.SV)
     seq += schedule_phase(cfg, sdp_mfmas(cfg, 0), [ds_part(cfg, 1, PART2), conv], f"P1.{p}", log)
     seq += stamp(cfg.SV)
+    # staging loads of tile j+2: K (regs free since P1's convert) then V (free since P2's),
+    # spread over P2, P3, P4
+    if "nospread" in asmgen.ABL:
+        ld = (staging_loads(cfg, 0), [], staging_loads(cfg, 1))
+    else:
+        ld = thirds(staging_loads(cfg, 0) + staging_loads(cfg, 1))
     seq += schedule_phase(cfg, dq_mfmas(cfg, 1), [ds_part(cfg, 0, PART1), staging_convert(cfg, 1, q),
-                                                  staging_loads(cfg, 0)], f"P2.{p}", log)
+                                                  list(ld[0])], f"P2.{p}", log)
     seq += stamp(cfg.SV)
-    seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [ds_part(cfg, 0, PART2), kt_all(cfg, p)], f"P3.{p}", log)
+    seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [ds_part(cfg, 0, PART2), kt_all(cfg, p), list(ld[1])], f"P3.{p}", log)
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     seq += stamp(cfg.SV)
     seq.append(tagged("bar", [Ins("s_barrier", "bar")])[0])
     seq += stamp(cfg.SV)
     seq += schedule_phase(cfg, dq_mfmas(cfg, 0), [ds_part(cfg, 1, PART1), row_reads(cfg, q, 0) + row_reads(cfg, q, 1),
-                                                  staging_loads(cfg, 1) + [goff_inc(cfg)]], f"P4.{p}", log)
+                                                  list(ld[2]) + [goff_inc(cfg)]], f"P4.{p}", log)
     return seq
 
 
