@@ -492,6 +492,19 @@ class Wave:
                 else:
                     y = np.maximum.reduce(xs)
                 self.put(f, k, f2u(y))
+            elif op in ("v_pk_add_f16", "v_pk_mul_f16"):
+                (f, k), = self.regs(args[0])
+                x, y = self.vsrc(args[1]), self.vsrc(args[2])
+                h = lambda u, sh: ((u >> sh) & 0xFFFF).astype(np.uint16).view(np.float16)
+                fn = (lambda a, b: a + b) if op == "v_pk_add_f16" else (lambda a, b: a * b)
+                lo = fn(h(x, 0), h(y, 0)).astype(np.float16).view(np.uint16).astype(np.uint32)
+                hi = fn(h(x, 16), h(y, 16)).astype(np.float16).view(np.uint16).astype(np.uint32)
+                self.put(f, k, lo | (hi << 16))
+            elif op in ("v_cvt_f32_f16_e32", "v_cvt_f32_f16_sdwa"):
+                (f, k), = self.regs(args[0])
+                x = self.vsrc(args[1].split()[0])
+                sh = 16 if op.endswith("sdwa") and "src0_sel:WORD_1" in ln else 0
+                self.put(f, k, f2u(((x >> sh) & 0xFFFF).astype(np.uint16).view(np.float16).astype(np.float32)))
             elif op == "v_add_u32":
                 (f, k), = self.regs(args[0])
                 self.put(f, k, (self.vsrc(args[1]).astype(np.uint64) + self.vsrc(args[2])).astype(np.uint32))

@@ -64,6 +64,10 @@ class Cfg:
         self.OST = D + 4
         self.mf = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvt = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
+        # fp16: dS = P * dP' on the packed 16-bit halves (v_pk_mul_f16, the 8-wave kernel's
+        # form): P and dP' packed first, one multiply per two products -- 20 instructions per
+        # 8 scores instead of 24; bf16 multiplies in fp32 ('pkmul32' build: fp16 too)
+        self.pkmul = not bf16 and "pkmul32" not in asmgen.ABL
         self.nvgpr, self.nagpr = 226, 256
 
     # AGPRs
@@ -204,6 +208,15 @@ def pds_part(cfg, qb, kb):
         for i in range(g0, g0 + 8):
             r = cfg.S(qb, kb, i)
             out.append(valu(f"v_exp_f32 v{r}, v{r}", [f"v{r}"], [f"v{r}"], kind="exp"))
+        if cfg.pkmul:
+            for base in (cfg.S(qb, kb, g0), cfg.dP(qb, kb, g0)):
+                for ii in range(4):
+                    d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
+                    out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
+            for ii in range(4):
+                r, d = cfg.S(qb, kb, g0 + ii), cfg.dP(qb, kb, g0 + ii)
+                out.append(valu(f"v_pk_mul_f16 v{d}, v{d}, v{r}", [f"v{d}", f"v{r}"], [f"v{d}"]))
+            continue
         for i in range(g0, g0 + 8):
             r, d = cfg.S(qb, kb, i), cfg.dP(qb, kb, i)
             out.append(valu(f"v_mul_f32 v{d}, v{d}, v{r}", [f"v{d}", f"v{r}"], [f"v{d}"]))

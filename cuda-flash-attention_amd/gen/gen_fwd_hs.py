@@ -81,6 +81,12 @@ class Cfg:
         self.mf = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvt = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
         self.exp_per_gap = 2 if D <= 64 else 1
+        # fp16 tiles: the row sums add the packed 16-bit P (v_pk_add_f16, two sums per add,
+        # issued like v_add_f32) into four packed partials per chain and tile, then one fp32
+        # add per lane half: 19 instructions per chain and tile instead of 40.  Five 16-bit
+        # roundings on sums of at most 16 P; bf16 (8-bit mantissa) keeps fp32 adds, as does
+        # the 'vsum' build
+        self.pksum = not bf16 and "vsum" not in asmgen.ABL
 
     # AGPRs
     def O(self, c, b):
@@ -205,39 +211,64 @@ def softmax_part(cfg, c, kb, final):
     """exp2 of the 16 scores of half kb (in place), partial row sums, pack to 16-bit P (in place)"""
     out = []
     S = lambda i: cfg.S(c, kb, i)
+    T = [cfg.T(c, k) for k in range(4)]
     for s in range(2):
         for i in range(8 * s, 8 * s + 8):
             out.append(valu(f"v_exp_f32 v{S(i)}, v{S(i)}", [f"v{S(i)}"], [f"v{S(i)}"], kind="exp"))
+        if cfg.pksum:
+            for ii in range(4):
+                d, a, b = S(8 * s + ii), S(8 * s + 2 * ii), S(8 * s + 2 * ii + 1)
+                out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
+            # packed partials: T0, T1 from half 0's first group, T2, T3 from its second;
+            # half 1 adds one packed P into each
+            p = [S(8 * s + ii) for ii in range(4)]
+            if kb == 0:
+                for k, (x, y) in enumerate(((p[0], p[1]), (p[2], p[3]))):
+                    t = T[2 * s + k]
+                    out.append(valu(f"v_pk_add_f16 v{t}, v{x}, v{y}", [f"v{x}", f"v{y}"], [f"v{t}"]))
+            else:
+                for k in range(4):
+                    t = T[k]
+                    out.append(valu(f"v_pk_add_f16 v{t}, v{t}, v{p[k]}", [f"v{t}", f"v{p[k]}"], [f"v{t}"]))
+            continue
         if kb == 0 and s == 0:
             for k in range(4):
-                T = cfg.T(c, k)
-                out.append(valu(f"v_add_f32 v{T}, v{S(k)}, v{S(k + 4)}", [f"v{S(k)}", f"v{S(k + 4)}"], [f"v{T}"]))
+                out.append(valu(f"v_add_f32 v{T[k]}, v{S(k)}, v{S(k + 4)}", [f"v{S(k)}", f"v{S(k + 4)}"], [f"v{T[k]}"]))
         elif "addrr" in asmgen.ABL:
             # the same sums in the same order per partial, round robin over the partials
             for e0 in (0, 4):
                 for k in range(4):
-                    T, e = cfg.T(c, k), 8 * s + k + e0
-                    out.append(valu(f"v_add_f32 v{T}, v{T}, v{S(e)}", [f"v{T}", f"v{S(e)}"], [f"v{T}"]))
+                    e = 8 * s + k + e0
+                    out.append(valu(f"v_add_f32 v{T[k]}, v{T[k]}, v{S(e)}", [f"v{T[k]}", f"v{S(e)}"], [f"v{T[k]}"]))
         else:
             for k in range(4):
-                T = cfg.T(c, k)
                 for e in (8 * s + k, 8 * s + k + 4):
-                    out.append(valu(f"v_add_f32 v{T}, v{T}, v{S(e)}", [f"v{T}", f"v{S(e)}"], [f"v{T}"]))
+                    out.append(valu(f"v_add_f32 v{T[k]}, v{T[k]}, v{S(e)}", [f"v{T[k]}", f"v{S(e)}"], [f"v{T[k]}"]))
         for ii in range(4):
             d, a, b = S(8 * s + ii), S(8 * s + 2 * ii), S(8 * s + 2 * ii + 1)
             out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
     tagged("sm", out)
     if final:
-        T = [cfg.T(c, k) for k in range(4)]
         ts = cfg.ts(c)
-        out.append(valu(f"v_add_f32 v{T[0]}, v{T[0]}, v{T[1]}", [f"v{T[0]}", f"v{T[1]}"], [f"v{T[0]}"]))
-        out.append(valu(f"v_add_f32 v{T[2]}, v{T[2]}, v{T[3]}", [f"v{T[2]}", f"v{T[3]}"], [f"v{T[2]}"]))
-        out.append(valu(f"v_add_f32 v{ts}, v{T[0]}, v{T[2]}", [f"v{T[0]}", f"v{T[2]}"], [f"v{ts}"]))
+        n0 = len(out)
+        if cfg.pksum:
+            t1 = cfg.tmp(0) if c == 0 else cfg.tmp(1)
+            out.append(valu(f"v_pk_add_f16 v{T[0]}, v{T[0]}, v{T[1]}", [f"v{T[0]}", f"v{T[1]}"], [f"v{T[0]}"]))
+            out.append(valu(f"v_pk_add_f16 v{T[2]}, v{T[2]}, v{T[3]}", [f"v{T[2]}", f"v{T[3]}"], [f"v{T[2]}"]))
+            out.append(valu(f"v_pk_add_f16 v{T[0]}, v{T[0]}, v{T[2]}", [f"v{T[0]}", f"v{T[2]}"], [f"v{T[0]}"]))
+            out.append(valu(f"v_cvt_f32_f16_e32 v{ts}, v{T[0]}", [f"v{T[0]}"], [f"v{ts}"]))
+            out.append(valu(f"v_cvt_f32_f16_sdwa v{t1}, v{T[0]} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1",
+                            [f"v{T[0]}"], [f"v{t1}"]))
+            out.append(valu(f"v_add_f32 v{ts}, v{ts}, v{t1}", [f"v{ts}", f"v{t1}"], [f"v{ts}"]))
+        else:
+            out.append(valu(f"v_add_f32 v{T[0]}, v{T[0]}, v{T[1]}", [f"v{T[0]}", f"v{T[1]}"], [f"v{T[0]}"]))
+            out.append(valu(f"v_add_f32 v{T[2]}, v{T[2]}, v{T[3]}", [f"v{T[2]}", f"v{T[3]}"], [f"v{T[2]}"]))
+            out.append(valu(f"v_add_f32 v{ts}, v{T[0]}, v{T[2]}", [f"v{T[0]}", f"v{T[2]}"], [f"v{ts}"]))
         out.append(valu(f"v_add_f32 v{cfg.l(c)}, v{cfg.l(c)}, v{ts}", [f"v{cfg.l(c)}", f"v{ts}"], [f"v{cfg.l(c)}"]))
         # NaN or a half-row sum above 2^13 -> the block is recomputed by the robust path
         out.append(valu(f"v_cmp_nge_f32 vcc, {SUM_MAX_BITS:#x}, v{ts}", [f"v{ts}"], ["vcc"]))  # !(2^13 >= ts)
         out.append(Ins("s_or_b64 %[flg], %[flg], vcc", "salu", R(["vcc", "s:flg"]), ["s:flg"]))
-        out[-6:-1] = tagged("sm", out[-6:-1])
+        out[n0:-1] = tagged("sm", out[n0:-1])
         out[-1].tag = "flag"
     return out
 
