@@ -80,7 +80,14 @@ def schedule_phase(cfg, mfmas, streams, name, log):
     tot = [max(1, sum(i.cost for i in s)) for s in streams]
     done = [0] * len(streams)
     total = sum(sum(i.cost for i in s) for s in streams)
-    cap = max(getattr(cfg, "min_cap", 24), -(-total // max(1, nM)))
+    # exact-result schedule A/Bs: 'epgN' at most N v_exp per gap, 'capN' minimum gap budget N
+    epg, mcap = cfg.exp_per_gap, getattr(cfg, "min_cap", 24)
+    for a in ABL:
+        if a.startswith("epg"):
+            epg = int(a[3:])
+        elif a.startswith("cap"):
+            mcap = int(a[3:])
+    cap = max(mcap, -(-total // max(1, nM)))
     out = []
     for g in range(nM + 1):
         used = 0
@@ -95,7 +102,7 @@ def schedule_phase(cfg, mfmas, streams, name, log):
             else:
                 if g < nM and used >= cap:
                     break
-                ok = [k for k in cands if g == nM or not (streams[k][pos[k]].kind == "exp" and nexp >= cfg.exp_per_gap)]
+                ok = [k for k in cands if g == nM or not (streams[k][pos[k]].kind == "exp" and nexp >= epg)]
                 if not ok:
                     break
                 k = min(ok, key=lambda k: (done[k] / tot[k], k))
@@ -250,7 +257,7 @@ EXACT_ABL = {"addrr", "nospread", "vsum", "pkmul32"}  # variants that keep the p
 
 def ablate(seq):
     """drop the loop-body instructions the active ablations name"""
-    if not ABL - EXACT_ABL:
+    if not {a for a in ABL - EXACT_ABL if not a.startswith(("epg", "cap"))}:
         return seq
     out = []
     for i in seq:
