@@ -48,7 +48,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import asmgen  # noqa: E402
-from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, stamp, tagged, valu  # noqa: E402,E501
+from asmgen import Ins, R, ablate, ablate_waits, fix_hazards, insert_waits, rng, rtxt, schedule_phase, stamp, tagged, thirds, valu  # noqa: E402,E501
 
 KT = 64  # keys per tile
 NWAVE = 4
@@ -80,7 +80,12 @@ class Cfg:
         self.OST = D + 4  # O stage row stride (floats)
         self.mf = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
         self.cvt = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
-        self.exp_per_gap = 2 if D <= 64 else 1
+        # D = 128 (r05 A/B, C4 / B2_H16_S4096 / B4_H16_S2048: -1.2 / -0.9 / -1.2 % in one
+        # process, profiles/r05/d128/): up to 3 v_exp per gap, and the next tile's staging
+        # loads spread over P2-P4 (asmgen.thirds) instead of K in P2 and V in P4; D = 64
+        # measured +0.4..0.8 % with either and keeps 2 and the bunched loads
+        self.exp_per_gap = 2 if D <= 64 else 3
+        self.spread = D == 128
         # fp16 tiles: the row sums add the packed 16-bit P (v_pk_add_f16, two sums per add,
         # issued like v_add_f32) into four packed partials per chain and tile, then one fp32
         # add per lane half: 19 instructions per chain and tile instead of 40.  Five 16-bit
@@ -310,6 +315,9 @@ def body(cfg, p, log):
     """one 64-key tile j with parity p: K/V of tile j in slot p; tile j+1 staged into 1-p"""
     q = 1 - p
     NKF, NTQ = cfg.NKF, cfg.NTQ
+    # staging loads of tile j+2: K in P2 and V in P4 (D = 64), or spread over P2-P4 (D = 128)
+    ld = thirds(staging_loads(cfg, 0) + staging_loads(cfg, 1)) if cfg.spread else \
+        (staging_loads(cfg, 0), [], staging_loads(cfg, 1))
     ring = lambda f: cfg.Kr(f % cfg.ring)
     seq = []
     # P1: QKᵀ of chain A (tile j) | softmax B (j-1) second half, K fragments 8.. (D=128), stage K(j+1)
@@ -334,7 +342,7 @@ def body(cfg, p, log):
         vre += vfrag_reads(cfg, i, p, earliest=i + 2)
     rer = [] if cfg.keep_k else [kfrag_read(cfg, f, p, cfg.Kr(f)) for f in range(cfg.ring)]
     seq += schedule_phase(cfg, pv_mfmas(cfg, 1), [softmax_part(cfg, 0, 0, False), staging_convert(cfg, 1, q),
-                                                  staging_loads(cfg, 0), rer, vre], f"P2.{p}", log)
+                                                  ld[0], rer, vre], f"P2.{p}", log)
     # P3: QKᵀ of chain B (tile j) | softmax A (j) second half, K fragments 8.. (D=128), rest of V(j)
     kreads = []
     if not cfg.keep_k:
@@ -347,7 +355,8 @@ def body(cfg, p, log):
     for i in range(nsplit, cfg.NF):
         vre += vfrag_reads(cfg, i, p)
     seq += stamp(cfg.SV)
-    seq += schedule_phase(cfg, qk_mfmas(cfg, 1, ring), [softmax_part(cfg, 0, 1, True), kreads, vre], f"P3.{p}", log)
+    seq += schedule_phase(cfg, qk_mfmas(cfg, 1, ring), [softmax_part(cfg, 0, 1, True), kreads, vre, list(ld[1])],
+                          f"P3.{p}", log)
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     seq += stamp(cfg.SV)
     seq.append(Ins("s_barrier", "bar"))
@@ -355,7 +364,7 @@ def body(cfg, p, log):
     # P4: PV of chain A (tile j) | softmax B (j) first half, K(j+1) fragment prefetch, V(j+2) loads
     pre = [kfrag_read(cfg, f, q, cfg.Kr(f)) for f in range(min(cfg.ring, NKF))]
     seq += schedule_phase(cfg, pv_mfmas(cfg, 0), [softmax_part(cfg, 1, 0, False), pre,
-                                                  staging_loads(cfg, 1) + [goff_inc(cfg)]], f"P4.{p}", log)
+                                                  list(ld[2]) + [goff_inc(cfg)]], f"P4.{p}", log)
     return seq
 
 
