@@ -67,7 +67,8 @@ def log(*a):
 
 
 # kernel-name prefixes in the rocprofv3 PMC summary
-PMC_PREFIX = {"fwd": "fa2_fwd_f16", "dq": "fa2_bwd_dq_f16", "dkdv": "fa2_bwd_dkdv_f16", "bwd32": "fa2_bwd_f32"}
+PMC_PREFIX = {"fwd": ("fa2_fwd_f16", "fa2_fwd_hs"), "dq": ("fa2_bwd_dq_f16", "fa2_bwd_dq_hs"),
+              "dkdv": ("fa2_bwd_dkdv_f16", "fa2_bwd_dkdv_hs"), "bwd32": ("fa2_bwd_f32",)}
 
 
 def traffic_from_profile(kernel: str, D: int, S: int, heads: int, build_id: str, path: str | None = None):
@@ -89,7 +90,7 @@ def traffic_from_profile(kernel: str, D: int, S: int, heads: int, build_id: str,
         log(f"profiles/pmc_summary.json is of build {meta.get('build_id')}, the library is {build_id}: traffic null")
         return None
     for name, ent in summ.items():
-        if name.startswith(PMC_PREFIX.get(kernel, "?")) and (f"<{D}," in name or f"<{D}>" in name):
+        if name.startswith(PMC_PREFIX.get(kernel, ("?",))) and (f"<{D}," in name or f"<{D}>" in name):
             try:
                 return float(ent["hbm_bytes_per_launch"])
             except (KeyError, TypeError):

@@ -1715,10 +1715,15 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     if constexpr (D == 64) {
         // hand-scheduled kernel (r05): whole 64-query steps, and a grid of at least one
         // 256-key workgroup per CU.  DKDV_HS (tests and tools): 1 forces it (an error where
-        // it cannot serve), 0 disables it
-        // (default off: at C3 it measured 145 vs 138 us for the 8-wave 16x16x32 kernel, r05
-        // in-process A/B, profiles/r05/; it stays reachable for tests and A/Bs)
+        // it cannot serve), 0 disables it.  Default on fp16 tiles (its final r05 form
+        // against the 8-wave 16x16x32 kernel in one process: C3 134.2 vs 134.7 us,
+        // B2_H8_S4096 125.1 vs 125.2, B16_H16_S2048 529.3 vs 552.9, S = 8192 467.7 vs 470.6;
+        // profiles/r05/dkhs/); bf16 tiles keep the 8-wave kernel (not measured against it)
+#ifdef FA2_TILE_BF16
         const int hs = tune_knob("DKDV_HS", 0);
+#else
+        const int hs = tune_knob("DKDV_HS", -1);
+#endif
         const bool fits = S % 64 == 0 && S >= 128;
         if (hs == 1 && !fits) return hipErrorInvalidValue;
         const long hgrid = (long)bh * ((S + 255) / 256);

@@ -285,6 +285,12 @@ def test_bench_traffic_only_from_a_profile_of_the_loaded_build(tmp_path):
     assert bench.traffic_from_profile("dkdv", 64, 2048, 64, bid, str(p)) == 123.0
     assert bench.traffic_from_profile("dkdv", 64, 2048, 64, "0" * 16, str(p)) is None
     assert bench.traffic_from_profile("dkdv", 64, 4096, 64, bid, str(p)) is None
+    # the hand-scheduled kernels' entries count too (their names carry <D>)
+    summ2 = {"_meta": summ["_meta"], "fa2_bwd_dkdv_hs_kernel<64>": {"hbm_bytes_per_launch": 77.0},
+             "fa2_fwd_hs_kernel<64>": {"hbm_bytes_per_launch": 55.0}}
+    p.write_text(json.dumps(summ2))
+    assert bench.traffic_from_profile("dkdv", 64, 2048, 64, bid, str(p)) == 77.0
+    assert bench.traffic_from_profile("fwd", 64, 2048, 64, bid, str(p)) == 55.0
     summ["_meta"].pop("build_id")
     p.write_text(json.dumps(summ))
     assert bench.traffic_from_profile("dkdv", 64, 2048, 64, bid, str(p)) is None
