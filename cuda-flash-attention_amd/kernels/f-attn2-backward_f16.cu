@@ -1715,15 +1715,11 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     if constexpr (D == 64) {
         // hand-scheduled kernel (r05): whole 64-query steps, and a grid of at least one
         // 256-key workgroup per CU.  DKDV_HS (tests and tools): 1 forces it (an error where
-        // it cannot serve), 0 disables it.  Default on fp16 tiles (its final r05 form
-        // against the 8-wave 16x16x32 kernel in one process: C3 134.2 vs 134.7 us,
-        // B2_H8_S4096 125.1 vs 125.2, B16_H16_S2048 529.3 vs 552.9, S = 8192 467.7 vs 470.6;
-        // profiles/r05/dkhs/); bf16 tiles keep the 8-wave kernel (not measured against it)
-#ifdef FA2_TILE_BF16
+        // it cannot serve), 0 disables it.  Default off: alone it beats the 8-wave
+        // 16x16x32 kernel (C3 134.2 vs 134.7 us, B16_H16_S2048 529.3 vs 552.9; r05,
+        // profiles/r05/dkhs/), but the fwd + bwd step with it is 0.6-2.2 % slower
+        // (C3 dO = ones 0.2952 vs 0.2905 ms; profiles/r05/dkhs_ones/)
         const int hs = tune_knob("DKDV_HS", 0);
-#else
-        const int hs = tune_knob("DKDV_HS", -1);
-#endif
         const bool fits = S % 64 == 0 && S >= 128;
         if (hs == 1 && !fits) return hipErrorInvalidValue;
         const long hgrid = (long)bh * ((S + 255) / 256);
