@@ -54,11 +54,10 @@ class Cfg:
         assert D == 64
         self.D, self.bf16 = D, bf16
         self.NB, self.NTQ, self.CPT = D // 32, D // 16, D // 32
-        # up to 2 v_exp per gap and a gap budget from 16 issue cycles (r05 A/B, fp16 in one
-        # process: -0.4 % at C3, -4.3 % at B16_H16_S2048, -0.5 % at S = 8192 against the 1 /
-        # 24 schedule; profiles/r05/dkhs/)
-        self.exp_per_gap = 2
-        self.min_cap = 16
+        # (2 v_exp per gap with a gap budget from 16 cycles: -0.4 % at C3, -4.3 % at
+        # B16_H16_S2048 alone, profiles/r05/dkhs/; kept at 1 / 24 while the kernel is opt-in:
+        # inside the step it loses either way, profiles/r05/dkhs_ones/)
+        self.exp_per_gap = 1
         self.TBB = QT * D * 2  # one 16-bit [64][D] tile
         # a slot: Q, dO tiles + row constants -LSE*log2e, -Delta (and a 256-B sink that waves
         # 2 and 3 write: every wave runs the same staging code)
