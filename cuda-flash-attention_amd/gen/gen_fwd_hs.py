@@ -86,6 +86,10 @@ class Cfg:
         # measured +0.4..0.8 % with either and keeps 2 and the bunched loads
         self.exp_per_gap = 2 if D <= 64 else 3
         self.spread = D == 128
+        # D = 128: per-gap issue budget from 16 cycles (was 24): C4 -0.4 %, B2_H16_S4096
+        # -0.4 %, B4_H16_S2048 -0.6 % in one process (profiles/r05/d128b/, 'cap16')
+        if D == 128:
+            self.min_cap = 16
         # fp16 tiles: the row sums add the packed 16-bit P (v_pk_add_f16, two sums per add,
         # issued like v_add_f32) into four packed partials per chain and tile, then one fp32
         # add per lane half: 19 instructions per chain and tile instead of 40.  Five 16-bit
