@@ -271,13 +271,12 @@ class Sim:
             self.lds[(cfg.RC >> 2) + q] = f2u(np.float32(-LSE[q] * LOG2E if ok else 0.0))
             self.lds[(cfg.RC >> 2) + 64 + q] = f2u(np.float32(-Delta[q] if ok else 0.0))
         lanes = np.arange(64)
-        r, h = lanes & 31, lanes >> 5
         g, i16 = lanes >> 4, lanes & 15
-        ka = [np.array([2 * tile_off(D, int(r[l]), 16 * t + 8 * int(h[l])) for l in lanes]) for t in range(D // 16)]
-        rt = 4 * (g >> 1) + (i16 >> 2)
-        ct = 16 * (g & 1) + 4 * (i16 & 3)
-        tr = [[np.array([2 * tile_off(D, int(rt[l]) + 8 * k, 32 * b + int(ct[l])) for l in lanes]) for k in range(2)]
-              for b in range(D // 32)]
+        # 16x16x32 maps (FragOffsets16): row reads row l & 15, columns 32 ks + 8g; transposed
+        # reads rows 16k + 4g + (i >> 2), columns 16 md + 4 (i & 3)
+        ka = [np.array([2 * tile_off(D, int(i16[l]), 32 * ks + 8 * int(g[l])) for l in lanes]) for ks in range(D // 32)]
+        tr = [[np.array([2 * tile_off(D, 16 * k + 4 * int(g[l]) + (int(i16[l]) >> 2), 16 * md + 4 * (int(i16[l]) & 3))
+                         for l in lanes]) for k in range(2)] for md in range(D // 16)]
         text = self.asm_text("fa2_bwd_dkdv_hs.inc", "FA2_DK_ASM")
         waves = []
         for w in range(4):
@@ -290,15 +289,15 @@ class Sim:
                 vo.append((row * D + ch * 8) * 4)
                 if c == 0:
                     lo = 2 * np.array([row[l] * D + ((ch[l] ^ SWZ[0](D, int(row[l]))) << 3) for l in lanes])
-            oak = ((w * 64 + r) * cfg.OST + 4 * h) * 4
-            ops = {"cnt": self.S // 64 - 1, "goff": 64 * D * 4, "roff": 256, "lo": lo, "rco": 16 * h,
+            oak = ((w * 64 + i16) * cfg.OST + 4 * g) * 4
+            ops = {"cnt": self.S // 64 - 1, "goff": 64 * D * 4, "roff": 256, "lo": lo, "rco": 16 * g,
                    "rvo": 4 * lanes, "rcw": (256 * w if w < 2 else 512) + 4 * lanes, "oak": oak,
                    "oav": oak + 256 * cfg.OST * 4, "rsq": "Q", "rsd": "dO",
                    "rsc": ["LSE", "Delta", "null", "null"][w],
                    "rsm": int(f2u(np.float32([-LOG2E, -1.0, 0.0, 0.0][w]))), "kvb": cfg.KVB + w * 64 * D * 2}
-            for t in range(D // 16):
+            for t in range(D // 32):
                 ops[f"ka{t}"] = ka[t]
-            for b in range(D // 32):
+            for b in range(D // 16):
                 for k in range(2):
                     ops[f"tr{b}_{k}"] = tr[b][k]
             for c in range(D // 32):

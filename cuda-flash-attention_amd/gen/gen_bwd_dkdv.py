@@ -8,33 +8,42 @@ C++ epilogue (dK, dV rows from an LDS stage; dK times 1/sqrt(D)).  The math is t
 part of the reference's backward (kernels/f-attn2-backward_f16.cu:170-268):
 P = exp(Q K^T / sqrt(D) - LSE), dV = P^T dO, dS = P o (dO V^T - Delta), dK = dS^T Q / sqrt(D):
 
-  * one workgroup = 4 waves = 256 keys, ONE wave per SIMD; each wave holds 64 keys (two
-    32-key blocks kb): their K and V fragments and dK^T / dV^T accumulators sit in AGPRs
+  * one workgroup = 4 waves = 256 keys, ONE wave per SIMD; each wave holds 64 keys (four
+    16-key blocks nb): their K and V fragments and dK^T / dV^T accumulators sit in AGPRs
     for the whole query loop;
   * the head's queries stream in 64-row steps (Q and dO as fp16/bf16 tiles, -LSE*log2e and
     -Delta rows) through a 3-slot LDS ring, one barrier per step.  The step's two 32-row
-    query blocks are the two chains A and B (r05: chains split by query, not by key, so
-    every transposed dO^T / Q^T fragment and every row-constant tuple is read once per
-    step, by the one chain it belongs to); per step four phases:
-        P1  S, dP of A (step j)        | P, dS of B (step j-1), key block 1
-        P2  dV^T, dK^T of B (step j-1)| P, dS of A (step j),   key block 0
-        P3  S, dP of B (step j)        | P, dS of A (step j),   key block 1   -> barrier
-        P4  dV^T, dK^T of A (step j)  | P, dS of B (step j),   key block 0
-  * S = Q K^T starts from -LSE*log2e and dP = dO V^T from -Delta (16-register row-constant
-    tuples read from LDS into a 2-slot ring: the query is on the accumulator rows), so
-    P = exp2(acc) and dS = P * acc; P and dS are packed in place and ARE the B operands
-    of dV^T += dO^T P and dK^T += Q^T dS (dO^T, Q^T through ds_read_b64_tr_b16 into an
-    8-slot ring);
+    query blocks are the two chains A and B (every transposed dO^T / Q^T fragment and
+    every row-constant tuple is read once per step, by the one chain it belongs to); per
+    step four phases:
+        P1  S, dP of A (step j)        | P, dS of B (step j-1), key blocks 2, 3
+        P2  dV^T, dK^T of B (step j-1)| P, dS of A (step j),   key blocks 0, 1
+        P3  S, dP of B (step j)        | P, dS of A (step j),   key blocks 2, 3   -> barrier
+        P4  dV^T, dK^T of A (step j)  | P, dS of B (step j),   key blocks 0, 1
+  * S = Q K^T starts from -LSE*log2e and dP = dO V^T from -Delta (4-register row-constant
+    tuples read from LDS: the query is on the accumulator rows), so P = exp2(acc) and
+    dS = P * acc; P and dS are packed in place and ARE the B operands of dV^T += dO^T P
+    and dK^T += Q^T dS (dO^T, Q^T through ds_read_b64_tr_b16 into an 8-fragment ring);
   * Q and dO rows: fp32 HBM -> registers -> fp16/bf16 -> swizzled LDS two steps ahead of
     their use; the row constants by one dword load per lane of waves 0 (LSE) and 1 (Delta).
+  * every product on v_mfma_f32_16x16x32 (r06; the r05 form of this loop ran 32x32x16 and
+    measured level with the compiler-scheduled 8-wave kernel: its MFMAs cost 15 % more
+    energy per FLOP at the power cap, where the kernel runs), on the operand maps
+      A[m = l & 15][k = 8g + j], B[k = 8g + j][n = l & 15], C[m = 4g + i][n = l & 15]  (g = l >> 4):
+    S / dP [16 queries mb][16 keys nb]: A = Q / dO rows 32 qb + 16 mb + (l & 15) (row
+    reads), B = K / V fragments of key 16 nb + (l & 15); dV^T / dK^T [16 d md][16 keys nb]
+    over the chain's 32 queries per MFMA: B = the packed P / dS of the chain's two query
+    blocks, k-slot 8g + j <-> query 16 (j >> 2) + 4g + (j & 3); A = dO^T / Q^T by two 4-row
+    transposed reads (rows 4g.. and 16 + 4g.., columns 16 md ..) in the same query order.
 
-Register map (D = 64):
-  AGPR  dK^T[kb][b] a[16(2kb+b)]  dV^T[kb][b] a[64+16(2kb+b)]
-        K[kb][t]   a[128+4(4kb+t)] V[kb][t]  a[160+4(4kb+t)]
-        Q rows     a[192+4(4qb+t)] dO rows   a[224+4(4qb+t)]
-  VGPR  S[qb][kb]  v[32qb+16kb]   dP[qb][kb] v[64+32qb+16kb]   (qb = the chain)
-        seed ring  v[128..159] (the chain's -LSE*log2e, -Delta tuples)
-        trop ring  v[160..191] (the chain's 8 dO^T / Q^T fragments)   staging v[192..223]  row const v[224]
+Register map (D = 64; qb the chain, mb its 16-query blocks, nb 16-key blocks, md 16-d blocks):
+  AGPR  dK^T[md][nb] a[4(4md + nb)]   dV^T[md][nb] a[64 + 4(4md + nb)]
+        K[nb][ks] a[128 + 4(2nb + ks)] V[nb][ks] a[160 + 4(2nb + ks)]
+        Q rows[qb][mb][ks] a[192 + 4(4qb + 2mb + ks)]   dO rows a[224 + ...]
+  VGPR  S[qb][nb][mb] v[32qb + 8nb + 4mb]  dP v[64 + ...]   (the two mb tuples of a key block
+        adjacent: packed in place into the key block's 4-register B operand)
+        seeds v[128 + 16qb + 8which + 4mb] (-LSE*log2e, -Delta tuples of each chain)
+        trop ring v[160..191] (a chain's 8 dO^T / Q^T fragments)   staging v[192..223]  row const v[224]
 
 Usage: python3 gen_bwd_dkdv.py [--check]
 """
@@ -53,11 +62,9 @@ class Cfg:
     def __init__(self, D, bf16):
         assert D == 64
         self.D, self.bf16 = D, bf16
-        self.NB, self.NTQ, self.CPT = D // 32, D // 16, D // 32
-        # (2 v_exp per gap with a gap budget from 16 cycles: -0.4 % at C3, -4.3 % at
-        # B16_H16_S2048 alone, profiles/r05/dkhs/; kept at 1 / 24 while the kernel is opt-in:
-        # inside the step it loses either way, profiles/r05/dkhs_ones/)
+        self.KS, self.NMD, self.NB, self.CPT = D // 32, D // 16, 4, D // 32
         self.exp_per_gap = 1
+        self.min_cap = 12  # 16-cycle MFMAs (gen_bwd_dq.py)
         self.TBB = QT * D * 2  # one 16-bit [64][D] tile
         # a slot: Q, dO tiles + row constants -LSE*log2e, -Delta (and a 256-B sink that waves
         # 2 and 3 write: every wave runs the same staging code)
@@ -65,42 +72,41 @@ class Cfg:
         self.RC = 2 * self.TBB  # row constants inside a slot
         self.KVB = 3 * self.SLOT  # K block, then V block (256 rows each)
         self.OST = D + 4
-        self.mf = "v_mfma_f32_32x32x16_bf16" if bf16 else "v_mfma_f32_32x32x16_f16"
+        self.mf = "v_mfma_f32_16x16x32_bf16" if bf16 else "v_mfma_f32_16x16x32_f16"
         self.cvt = "v_cvt_pk_bf16_f32" if bf16 else "v_cvt_pk_f16_f32"
-        # fp16: dS = P * dP' on the packed 16-bit halves (v_pk_mul_f16, the 8-wave kernel's
-        # form): P and dP' packed first, one multiply per two products -- 20 instructions per
-        # 8 scores instead of 24; bf16 multiplies in fp32 ('pkmul32' build: fp16 too)
+        # fp16: dS = P * dP' on the packed 16-bit halves (v_pk_mul_f16): P and dP' packed
+        # first, one multiply per two products; bf16 multiplies in fp32 ('pkmul32': fp16 too)
         self.pkmul = not bf16 and "pkmul32" not in asmgen.ABL
         self.nvgpr, self.nagpr = 226, 256
 
     # AGPRs
-    def dK(self, c, b):
-        return 16 * (2 * c + b)
+    def dK(self, md, nb):
+        return 4 * (4 * md + nb)
 
-    def dV(self, c, b):
-        return 64 + 16 * (2 * c + b)
+    def dV(self, md, nb):
+        return 64 + 4 * (4 * md + nb)
 
-    def Kf(self, c, t):
-        return 128 + 4 * (4 * c + t)
+    def Kf(self, nb, ks):
+        return 128 + 4 * (2 * nb + ks)
 
-    def Vf(self, c, t):
-        return 160 + 4 * (4 * c + t)
+    def Vf(self, nb, ks):
+        return 160 + 4 * (2 * nb + ks)
 
-    def Qr(self, qb, t):
-        return 192 + 4 * (4 * qb + t)
+    def Qr(self, qb, mb, ks):
+        return 192 + 4 * (4 * qb + 2 * mb + ks)
 
-    def dOr(self, qb, t):
-        return 224 + 4 * (4 * qb + t)
+    def dOr(self, qb, mb, ks):
+        return 224 + 4 * (4 * qb + 2 * mb + ks)
 
     # VGPRs
-    def S(self, qb, kb, i=0):
-        return 32 * qb + 16 * kb + i
+    def S(self, qb, nb, mb=0, i=0):
+        return 32 * qb + 8 * nb + 4 * mb + i
 
-    def dP(self, qb, kb, i=0):
-        return 64 + 32 * qb + 16 * kb + i
+    def dP(self, qb, nb, mb=0, i=0):
+        return 64 + 32 * qb + 8 * nb + 4 * mb + i
 
-    def seed(self, k):
-        return 128 + 16 * k
+    def seed(self, qb, which, mb):
+        return 128 + 16 * qb + 8 * which + 4 * mb
 
     def tr(self, k):
         return 160 + 4 * k
@@ -119,111 +125,110 @@ class Cfg:
 def mfma(cfg, dst, a, b, c, c_is_zero=False):
     rd = R(rng(a[0], a[1], 4), "A") + R(rng(b[0], b[1], 4), "B")
     if not c_is_zero:
-        rd += R(rng(c[0], c[1], 16), "C")
-    ctxt = "0" if c_is_zero else rtxt(c[0], c[1], 16)
-    return Ins(f"{cfg.mf} {rtxt(dst[0], dst[1], 16)}, {rtxt(a[0], a[1], 4)}, {rtxt(b[0], b[1], 4)}, {ctxt}", "mfma",
-               rd, rng(dst[0], dst[1], 16))
+        rd += R(rng(c[0], c[1], 4), "C")
+    ctxt = "0" if c_is_zero else rtxt(c[0], c[1], 4)
+    return Ins(f"{cfg.mf} {rtxt(dst[0], dst[1], 4)}, {rtxt(a[0], a[1], 4)}, {rtxt(b[0], b[1], 4)}, {ctxt}", "mfma",
+               rd, rng(dst[0], dst[1], 4))
 
 
 # ---- LDS reads --------------------------------------------------------------------------
 def rowop_reads(cfg, slot):
-    """Q and dO row fragments (qb, t) of the step in `slot` -> AGPRs (A operands of S, dP)"""
+    """Q and dO row fragments (qb, mb, ks) of the step in `slot` -> AGPRs (A operands of S, dP);
+    chain A's first (chain B's S, dP of the step before may still be reading theirs)"""
     out = []
-    for tensor in range(2):
-        for qb in range(2):
-            for t in range(cfg.NTQ):
-                d = cfg.Qr(qb, t) if tensor == 0 else cfg.dOr(qb, t)
-                off = slot * cfg.SLOT + tensor * cfg.TBB + qb * 32 * cfg.D * 2
-                out.append(Ins(f"ds_read_b128 {rtxt('a', d, 4)}, %[ka{t}] offset:{off}", "dsr", [], rng("a", d, 4)))
+    for qb in range(2):
+        for tensor in range(2):
+            for mb in range(2):
+                for ks in range(cfg.KS):
+                    d = cfg.Qr(qb, mb, ks) if tensor == 0 else cfg.dOr(qb, mb, ks)
+                    off = slot * cfg.SLOT + tensor * cfg.TBB + (32 * qb + 16 * mb) * cfg.D * 2
+                    out.append(Ins(f"ds_read_b128 {rtxt('a', d, 4)}, %[ka{ks}] offset:{off}", "dsr", [],
+                                   rng("a", d, 4), earliest=qb))
     return tagged("lds", out)
 
 
-def seed_reads(cfg, slot, which, qb, k, earliest=0, deadline=None):
-    """row-constant tuple (which 0: -LSE*log2e, 1: -Delta) of query block qb -> seed ring slot k:
-    register 4g+e holds the row qb*32 + 8g + 4h + e"""
+def seed_reads(cfg, slot, which, qb, earliest=0, deadline=None):
+    """row-constant tuples (which 0: -LSE*log2e, 1: -Delta) of chain qb: register i of the
+    tuple of query block mb holds row 32 qb + 16 mb + 4g + i"""
     out = []
-    base = slot * cfg.SLOT + cfg.RC + which * 256 + qb * 128
-    d = cfg.seed(k)
-    for g in range(4):
-        out.append(Ins(f"ds_read_b128 {rtxt('v', d + 4 * g, 4)}, %[rco] offset:{base + 32 * g}", "dsr", [],
-                       rng("v", d + 4 * g, 4), earliest=earliest, deadline=deadline))
+    for mb in range(2):
+        off = slot * cfg.SLOT + cfg.RC + which * 256 + (32 * qb + 16 * mb) * 4
+        d = cfg.seed(qb, which, mb)
+        out.append(Ins(f"ds_read_b128 {rtxt('v', d, 4)}, %[rco] offset:{off}", "dsr", [], rng("v", d, 4),
+                       earliest=earliest, deadline=deadline))
     return tagged("lds", out)
 
 
-def trop_frag(cfg, k):
-    """the k-th A operand of a chain's dV^T / dK^T phase: (tensor, b, s)"""
-    tensor = k // 4  # 0: dO^T (for dV), 1: Q^T (for dK)
-    b, s = (k % 4) // 2, k % 2
-    return tensor, b, s
+def trop_frag(k):
+    """the k-th A operand of a chain's dV^T / dK^T phase: (tensor 0: dO^T, 1: Q^T; md)"""
+    return k // 4, k % 4
 
 
 def trop_reads(cfg, slot, qb, k, earliest=0, deadline=None):
-    tensor, b, s = trop_frag(cfg, k)
+    tensor, md = trop_frag(k)
     tt = 1 if tensor == 0 else 0  # LDS tile: 0 = Q, 1 = dO
-    off = slot * cfg.SLOT + tt * cfg.TBB + (qb * 32 + 16 * s) * cfg.D * 2
+    off = slot * cfg.SLOT + tt * cfg.TBB + 32 * qb * cfg.D * 2
     d = cfg.tr(k)
     return tagged("lds", [
-        Ins(f"ds_read_b64_tr_b16 {rtxt('v', d, 2)}, %[tr{b}_0] offset:{off}", "dsr", [], rng("v", d, 2),
+        Ins(f"ds_read_b64_tr_b16 {rtxt('v', d, 2)}, %[tr{md}_0] offset:{off}", "dsr", [], rng("v", d, 2),
             earliest=earliest, deadline=deadline),
-        Ins(f"ds_read_b64_tr_b16 {rtxt('v', d + 2, 2)}, %[tr{b}_1] offset:{off}", "dsr", [], rng("v", d + 2, 2),
+        Ins(f"ds_read_b64_tr_b16 {rtxt('v', d + 2, 2)}, %[tr{md}_1] offset:{off}", "dsr", [], rng("v", d + 2, 2),
             earliest=earliest, deadline=deadline)])
 
 
 # ---- MFMA chains -------------------------------------------------------------------------
-SEED_ORDER = [(0, 0, 0), (1, 0, 1), (0, 1, 0), (1, 1, 1)]  # (which, kb, seed ring slot) in MFMA order
-
-
 def sdp_mfmas(cfg, qb):
-    """chain qb: S[qb][kb] = Q K^T - LSE*log2e, dP[qb][kb] = dO V^T - Delta; S kb0, dP kb0, S kb1,
-    dP kb1 (key block 0 first: its P, dS are the next phase's filler)"""
+    """chain qb: S[qb][nb][mb] = Q K^T - LSE*log2e, dP = dO V^T - Delta; key blocks 0, 1 first
+    (their P, dS are the next phase's filler)"""
     out = []
-    for which, kb, k in SEED_ORDER:
-        for t in range(cfg.NTQ):
-            if which == 0:
-                dst, a, b = cfg.S(qb, kb), cfg.Qr(qb, t), cfg.Kf(kb, t)
-            else:
-                dst, a, b = cfg.dP(qb, kb), cfg.dOr(qb, t), cfg.Vf(kb, t)
-            cc = ("v", cfg.seed(k)) if t == 0 else ("v", dst)
-            out.append(mfma(cfg, ("v", dst), ("a", a), ("a", b), cc))
+    for nb in range(cfg.NB):
+        for mb in range(2):
+            for which in range(2):
+                for ks in range(cfg.KS):
+                    if which == 0:
+                        dst, a, b = cfg.S(qb, nb, mb), cfg.Qr(qb, mb, ks), cfg.Kf(nb, ks)
+                    else:
+                        dst, a, b = cfg.dP(qb, nb, mb), cfg.dOr(qb, mb, ks), cfg.Vf(nb, ks)
+                    cc = ("v", cfg.seed(qb, which, mb)) if ks == 0 else ("v", dst)
+                    out.append(mfma(cfg, ("v", dst), ("a", a), ("a", b), cc))
     return out
 
 
 def dkdv_mfmas(cfg, qb, first=False):
-    """chain qb's share: dV^T[kb][b] += dO^T P[qb][kb], dK^T[kb][b] += Q^T dS[qb][kb]; trop ring
-    slot k (fragment k of the chain) feeds the two key blocks back to back"""
+    """chain qb's share: dV^T[md][nb] += dO^T P[qb][nb], dK^T[md][nb] += Q^T dS[qb][nb]; trop
+    ring fragment k feeds the four key blocks back to back"""
     out = []
     for k in range(8):
-        tensor, b, s = trop_frag(cfg, k)
-        for kb in range(2):
-            acc = cfg.dV(kb, b) if tensor == 0 else cfg.dK(kb, b)
-            src = cfg.S(qb, kb, 8 * s) if tensor == 0 else cfg.dP(qb, kb, 8 * s)
-            z = first and s == 0
-            out.append(mfma(cfg, ("a", acc), ("v", cfg.tr(k)), ("v", src), ("a", acc), c_is_zero=z))
+        tensor, md = trop_frag(k)
+        for nb in range(cfg.NB):
+            acc = cfg.dV(md, nb) if tensor == 0 else cfg.dK(md, nb)
+            src = cfg.S(qb, nb) if tensor == 0 else cfg.dP(qb, nb)
+            out.append(mfma(cfg, ("a", acc), ("v", cfg.tr(k)), ("v", src), ("a", acc), c_is_zero=first))
     return out
 
 
 # ---- VALU ---------------------------------------------------------------------------------
-def pds_part(cfg, qb, kb):
-    """P = exp2(S) and dS = P * dP' of key block kb of chain qb, packed in place"""
+def pds_part(cfg, qb, half):
+    """P = exp2(S) and dS = P * dP' of key blocks 2 half, 2 half + 1 of chain qb, packed in
+    place (register 2ii of the pair (2ii, 2ii + 1) -> ii: the B operand order above)"""
     out = []
-    for s in range(2):
-        g0 = 8 * s
-        for i in range(g0, g0 + 8):
-            r = cfg.S(qb, kb, i)
-            out.append(valu(f"v_exp_f32 v{r}, v{r}", [f"v{r}"], [f"v{r}"], kind="exp"))
+    for nb in (2 * half, 2 * half + 1):
+        sb, db = cfg.S(qb, nb), cfg.dP(qb, nb)
+        for i in range(8):
+            out.append(valu(f"v_exp_f32 v{sb + i}, v{sb + i}", [f"v{sb + i}"], [f"v{sb + i}"], kind="exp"))
         if cfg.pkmul:
-            for base in (cfg.S(qb, kb, g0), cfg.dP(qb, kb, g0)):
+            for base in (sb, db):
                 for ii in range(4):
                     d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
                     out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
             for ii in range(4):
-                r, d = cfg.S(qb, kb, g0 + ii), cfg.dP(qb, kb, g0 + ii)
+                r, d = sb + ii, db + ii
                 out.append(valu(f"v_pk_mul_f16 v{d}, v{d}, v{r}", [f"v{d}", f"v{r}"], [f"v{d}"]))
             continue
-        for i in range(g0, g0 + 8):
-            r, d = cfg.S(qb, kb, i), cfg.dP(qb, kb, i)
+        for i in range(8):
+            r, d = sb + i, db + i
             out.append(valu(f"v_mul_f32 v{d}, v{d}, v{r}", [f"v{d}", f"v{r}"], [f"v{d}"]))
-        for base in (cfg.S(qb, kb, g0), cfg.dP(qb, kb, g0)):
+        for base in (sb, db):
             for ii in range(4):
                 d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
                 out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
@@ -270,7 +275,8 @@ def body(cfg, j3, log):
     chain B's dV/dK of step j-1 read slot (j3+2)%3"""
     s, n, pv = j3, (j3 + 1) % 3, (j3 + 2) % 3
     seq = []
-    # P1: S, dP of A | P, dS of B (j-1) key block 1; stage step j+1; B's (j-1) trop frags for P2
+    # P1: S, dP of A | P, dS of B (j-1) key blocks 2, 3; stage step j+1; B's (j-1) trop frags
+    #     for P2 (the ring is free once P4's first MFMAs have read A's)
     pre = []
     for k in range(8):
         pre += trop_reads(cfg, pv, 1, k, earliest=2)
@@ -278,11 +284,10 @@ def body(cfg, j3, log):
     for i in conv:
         i.earliest = 2
     seq += schedule_phase(cfg, sdp_mfmas(cfg, 0), [pds_part(cfg, 1, 1), conv, pre], f"P1.{j3}", log)
-    # P2: dV, dK of B (j-1) | P, dS of A key block 0; seeds of B for P3 (A's done with the ring);
-    #     loads of step j+2
-    sd = seed_reads(cfg, s, 0, 1, 0) + seed_reads(cfg, s, 1, 1, 1)
-    # loads of step j+2 (staging registers free since P1's convert) spread over P2, P3, P4;
-    # the offset adds after the last of them
+    # P2: dV, dK of B (j-1) | P, dS of A key blocks 0, 1; B's seeds for P3; loads of step j+2
+    #     (staging registers free since P1's convert) spread over P2, P3, P4, the offset adds
+    #     after the last of them
+    sd = seed_reads(cfg, s, 0, 1) + seed_reads(cfg, s, 1, 1)
     stl = staging_loads(cfg)
     if "nospread" in asmgen.ABL:
         ld = (stl, [], [])
@@ -290,67 +295,69 @@ def body(cfg, j3, log):
         ld = thirds(stl[:-2])
         ld = (ld[0], ld[1], ld[2] + stl[-2:])
     seq += schedule_phase(cfg, dkdv_mfmas(cfg, 1), [pds_part(cfg, 0, 0), sd, list(ld[0])], f"P2.{j3}", log)
-    # P3: S, dP of B | P, dS of A key block 1; A's trop frags for P4 (the ring is free after P2)
+    # P3: S, dP of B | P, dS of A key blocks 2, 3; A's trop frags for P4 (the ring is free
+    #     after P2)
     pre = []
     for k in range(8):
-        pre += trop_reads(cfg, s, 0, k)
+        pre += trop_reads(cfg, s, 0, k, earliest=2)
     seq += schedule_phase(cfg, sdp_mfmas(cfg, 1), [pds_part(cfg, 0, 1), pre, list(ld[1])], f"P3.{j3}", log)
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     seq.append(tagged("bar", [Ins("s_barrier", "bar")])[0])
-    # P4: dV, dK of A | P, dS of B key block 0; Q/dO rows and A's seeds of step j+1 (the seed
-    #     ring is free after P3)
-    nxt = rowop_reads(cfg, n) + seed_reads(cfg, n, 0, 0, 0, earliest=2) + seed_reads(cfg, n, 1, 0, 1, earliest=2)
+    # P4: dV, dK of A | P, dS of B key blocks 0, 1; Q/dO rows and A's seeds of step j+1
+    #     (staged before the barrier by every wave)
+    nxt = rowop_reads(cfg, n) + seed_reads(cfg, n, 0, 0, earliest=2) + seed_reads(cfg, n, 1, 0, earliest=2)
     seq += schedule_phase(cfg, dkdv_mfmas(cfg, 0), [pds_part(cfg, 1, 0), nxt, list(ld[2])], f"P4.{j3}", log)
     return seq
 
 
 def prologue(cfg):
-    """step 0 serially (both chains' S, dP; A's P, dS and dV, dK -- whose first MFMAs start
-    every accumulator from zero; B's first half), step 1 staged"""
-    D, NTQ = cfg.D, cfg.NTQ
+    """step 0 serially (both chains' S, dP; A's P, dS and dV, dK -- whose MFMAs start every
+    accumulator from zero; B's key blocks 0, 1), step 1 staged"""
+    D = cfg.D
     seq = staging_loads(cfg)  # step 1
-    # K and V fragments of both chains from the workgroup's K / V blocks (%[kvb]: this wave's rows)
-    for t in range(NTQ):
-        seq.append(valu(f"v_add_u32 v{t}, %[kvb], %[ka{t}]", [], [f"v{t}"]))
-    for c in range(2):
-        for t in range(NTQ):
-            seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.Kf(c, t), 4)}, v{t} offset:{c * 32 * D * 2}", "dsr",
-                           R([f"v{t}"]), rng("a", cfg.Kf(c, t), 4)))
-            seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.Vf(c, t), 4)}, v{t} offset:{KEYS * D * 2 + c * 32 * D * 2}",
-                           "dsr", R([f"v{t}"]), rng("a", cfg.Vf(c, t), 4)))
+    # K and V fragments of the wave's 64 keys from the workgroup's K / V blocks (%[kvb]: this
+    # wave's rows)
+    for ks in range(cfg.KS):
+        seq.append(valu(f"v_add_u32 v{ks}, %[kvb], %[ka{ks}]", [], [f"v{ks}"]))
+    for nb in range(cfg.NB):
+        for ks in range(cfg.KS):
+            seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.Kf(nb, ks), 4)}, v{ks} offset:{nb * 16 * D * 2}", "dsr",
+                           R([f"v{ks}"]), rng("a", cfg.Kf(nb, ks), 4)))
+            seq.append(Ins(f"ds_read_b128 {rtxt('a', cfg.Vf(nb, ks), 4)}, v{ks} offset:{KEYS * D * 2 + nb * 16 * D * 2}",
+                           "dsr", R([f"v{ks}"]), rng("a", cfg.Vf(nb, ks), 4)))
     seq += rowop_reads(cfg, 0)
     for qb in range(2):
-        seq += seed_reads(cfg, 0, 0, qb, 0) + seed_reads(cfg, 0, 1, qb, 1)
+        seq += seed_reads(cfg, 0, 0, qb) + seed_reads(cfg, 0, 1, qb)
         seq += sdp_mfmas(cfg, qb)
     seq += pds_part(cfg, 0, 0) + pds_part(cfg, 0, 1) + pds_part(cfg, 1, 0)
     mf = dkdv_mfmas(cfg, 0, first=True)
     for k in range(8):
         seq += trop_reads(cfg, 0, 0, k)
-        seq += mf[2 * k:2 * k + 2]
+        seq += mf[4 * k:4 * k + 4]
     seq += staging_convert(cfg, 1)
     seq += staging_loads(cfg)  # step 2
     seq += [Ins("s_waitcnt lgkmcnt(0)", "wait"), Ins("s_barrier", "bar")]
-    seq += rowop_reads(cfg, 1) + seed_reads(cfg, 1, 0, 0, 0) + seed_reads(cfg, 1, 1, 0, 1)
+    seq += rowop_reads(cfg, 1) + seed_reads(cfg, 1, 0, 0) + seed_reads(cfg, 1, 1, 0)
     return seq
 
 
 def epilogue(cfg, last_slot_expr):
-    """after the last step: B's second half, its dV, dK; stage dK^T, dV^T (last slot: the body
-    that exits passes its slot)"""
+    """after the last step: B's key blocks 2, 3, its dV, dK; stage dK^T, dV^T (last slot: the
+    body that exits passes its slot)"""
     seq = [Ins("s_waitcnt vmcnt(0) lgkmcnt(0)", "wait")]
     seq += pds_part(cfg, 1, 1)
     mf = dkdv_mfmas(cfg, 1)
     for k in range(8):
         seq += trop_reads(cfg, last_slot_expr, 1, k)
-        seq += mf[2 * k:2 * k + 2]
+        seq += mf[4 * k:4 * k + 4]
     seq.append(Ins("s_barrier", "bar"))
+    # dK^T[md][nb] register i: d = 16 md + 4g + i of key 16 nb + (l & 15) -> stage row, 4 columns
     for tensor, op in ((0, "%[oak]"), (1, "%[oav]")):
-        for c in range(2):  # key block
-            for b in range(cfg.NB):
-                for g in range(4):
-                    r = (cfg.dK(c, b) if tensor == 0 else cfg.dV(c, b)) + 4 * g
-                    off = (c * 32 * cfg.OST + 32 * b + 8 * g) * 4
-                    seq.append(Ins(f"ds_write_b128 {op}, {rtxt('a', r, 4)} offset:{off}", "dsw", R(rng("a", r, 4)), []))
+        for md in range(cfg.NMD):
+            for nb in range(cfg.NB):
+                r = cfg.dK(md, nb) if tensor == 0 else cfg.dV(md, nb)
+                off = (16 * nb * cfg.OST + 16 * md) * 4
+                seq.append(Ins(f"ds_write_b128 {op}, {rtxt('a', r, 4)} offset:{off}", "dsw", R(rng("a", r, 4)), []))
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     return seq
 
@@ -406,16 +413,17 @@ def build(cfg):
     allb = done[0] + done[1] + done[2]
     nm = sum(1 for i in allb if i.kind == "mfma")
     nv = sum(1 for i in allb if i.kind in ("valu", "exp"))
+    nl = sum(1 for i in allb if i.kind == "dsr")
     nn = sum(int(i.text.split()[1]) + 1 for i in allb if i.kind == "nop")
-    log.append(f"  loop (3 steps): {nm} MFMA, {nv} VALU ({nv / max(nm, 1):.2f} per MFMA), {nn} nop wait states, "
-               f"{len(allb)} instructions")
+    log.append(f"  loop (3 steps): {nm} MFMA, {nv} VALU ({nv / max(nm, 1):.2f} per MFMA), {nl} LDS reads "
+               f"({nl / max(nm, 1):.2f} per MFMA), {nn} nop wait states, {len(allb)} instructions")
     return lines, log
 
 
 def operands(cfg):
     outs = ['[cnt] "+s"(hs_cnt)', '[goff] "+s"(hs_goff)', '[roff] "+s"(hs_roff)']
-    ins = [f'[ka{t}] "v"(hs_ka[{t}])' for t in range(cfg.NTQ)]
-    ins += [f'[tr{b}_{k}] "v"(hs_tr[{b}][{k}])' for b in range(cfg.NB) for k in range(2)]
+    ins = [f'[ka{ks}] "v"(hs_ka[{ks}])' for ks in range(cfg.KS)]
+    ins += [f'[tr{md}_{k}] "v"(hs_tr[{md}][{k}])' for md in range(cfg.NMD) for k in range(2)]
     ins += [f'[vo{c}] "v"(hs_vo[{c}])' for c in range(cfg.CPT)]
     ins += ['[lo] "v"(hs_lo)', '[rco] "v"(hs_rco)', '[rvo] "v"(hs_rvo)', '[rcw] "v"(hs_rcw)', '[oak] "v"(hs_oak)',
             '[oav] "v"(hs_oav)', '[rsq] "s"(hs_rsq)', '[rsd] "s"(hs_rsd)', '[rsc] "s"(hs_rsc)', '[rsm] "s"(hs_rsm)',

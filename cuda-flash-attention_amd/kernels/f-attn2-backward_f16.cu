@@ -420,33 +420,21 @@ struct FragOffsets16 {
 // (`profiles/r03/ab/iglp/`): strategy 0 on dK/dV -1.3 % at C3 in three runs (step -0.6 %,
 // C5 and B2_H8_S4096 -0.5 %), +12 % slower at D = 32 (so D = 64 only); strategies 1-3
 // and any strategy on dQ within +-0.8 %.
-#ifndef FA2_IGLP_DKDV
-#define FA2_IGLP_DKDV 0
-#endif
-#ifndef FA2_IGLP_DQ
-#define FA2_IGLP_DQ -1
-#endif
+constexpr int kIglpDkdv = 0, kIglpDq = -1;
 // ... and for the fused small-grid backward: strategy 2 took B2_H8_S512 15.8 -> 15.3 us
 // (dO = ones) and 15.6 -> 15.1 (N(0,1)), S = 1024 fwd + bwd -1.5 %, B4_H8_S512, D = 32
 // and S = 2048 +-0; strategy 1 lost 4 % at S = 512.  Per role: the dK/dV role needs it
 // with split queries (S = 512: 16.0 us without), and with unsplit queries (4-8 blocks per
 // CU) strategy 0 is better (B2_H8_S2048 64.4 -> 62.7 us); the dQ role +-1 % either way.
-#ifndef FA2_IGLP_FUSED
-#define FA2_IGLP_FUSED 2
-#endif
+constexpr int kIglpFused = 2;
 template <int D, int IGLP = -1, typename Mid>
 __device__ __forceinline__ void dkdv_step16(DkdvState16<D>& st, const _Float16* Qs, const _Float16* dOs,
                                             const float* nlse2, const float* ndel, const FragOffsets16<D>& fo,
                                             int g, Mid&& mid) {
-#ifdef FA2_IGLP_DKDV_ONCE
-    if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
-#endif
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
         if (qb == 1) mid();
-#ifndef FA2_IGLP_DKDV_ONCE
         if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);  // LLVM scheduling strategy for the region
-#endif
         f32x4 sa[2][2], da[2][2];  // [mb][nb]
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb) {
@@ -811,7 +799,7 @@ fa2_bwd_dkdv_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K
                         const float* __restrict__ Delta, float* __restrict__ dK, float* __restrict__ dV, int S) {
     __shared__ __attribute__((aligned(16))) char lds[DkdvLds<D, NW, KB, QS>::BYTES];
     // the unsplit instances (full grids: C3, C5, long S) under an LLVM scheduling strategy
-    dkdv_body<D, NW, KB, M16, QS, false, QS == 1 && D == 64 ? FA2_IGLP_DKDV : -1>(lds, xcd_remap(blockIdx.x, gridDim.x),
+    dkdv_body<D, NW, KB, M16, QS, false, QS == 1 && D == 64 ? kIglpDkdv : -1>(lds, xcd_remap(blockIdx.x, gridDim.x),
                                                                                  Q, K, V, dO, LSE, Delta, dK, dV, S);
 }
 
@@ -1206,10 +1194,7 @@ __device__ __forceinline__ void dq_body(char* __restrict__ lds, int bid, const f
 // rows it leaves (unscaled fp32) in an LDS stage.  Every dQ element is summed in one fixed
 // order: bitwise reproducible, no atomics (the reference: f-attn2-backward_f16.cu:240-301).
 }  // namespace fa2f16b
-#ifndef FA2_DQ_INC
-#define FA2_DQ_INC "fa2_bwd_dq_hs.inc"  // (timing-only ablation builds name another, tools/r05_hs_abl.sh)
-#endif
-#include FA2_DQ_INC
+#include "fa2_bwd_dq_hs.inc"
 namespace fa2f16b {
 
 template <int D>
@@ -1328,10 +1313,7 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
 // dV leave through an LDS stage as whole rows (dK times 1/sqrt(D)); every element is
 // summed in one fixed order (the reference: f-attn2-backward_f16.cu:170-268).
 }  // namespace fa2f16b
-#ifndef FA2_DK_INC
-#define FA2_DK_INC "fa2_bwd_dkdv_hs.inc"  // (timing-only ablation builds name another, tools/r05_hs_abl.sh)
-#endif
-#include FA2_DK_INC
+#include "fa2_bwd_dkdv_hs.inc"
 namespace fa2f16b {
 
 template <int D>
@@ -1345,7 +1327,7 @@ fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K,
     __shared__ __attribute__((aligned(16))) char lds[FA2_DK_LDS_D64];
     _Float16* sh = reinterpret_cast<_Float16*>(lds);
 
-    const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nkb = (S + 255) / 256;
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -1382,22 +1364,26 @@ fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K,
     }
     __syncthreads();
 
-    FragOffsets<D> fo;
+    // per-lane LDS byte offsets of the row and transposed fragment reads (16x16x32 maps)
+    FragOffsets16<D> fo;
     fo.init(lane);
-    int hs_ka[D / 16], hs_tr[D / 32][2], hs_vo[D / 32];
+    int hs_ka[D / 32], hs_tr[D / 16][2], hs_vo[D / 32];
 #pragma unroll
-    for (int t = 0; t < D / 16; ++t) hs_ka[t] = fo.row[t] * 2;
+    for (int t = 0; t < D / 32; ++t) hs_ka[t] = fo.row[t] * 2;
 #pragma unroll
-    for (int b = 0; b < D / 32; ++b) {
+    for (int b = 0; b < D / 16; ++b) {
         hs_tr[b][0] = fo.tr[b][0] * 2;
         hs_tr[b][1] = fo.tr[b][1] * 2;
     }
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) hs_vo[c] = qs.voff[c];
     const int hs_lo = qs.loff[0] * 2;
-    const int hs_rco = 16 * h, hs_rvo = 4 * lane;
+    // row-constant tuples: rows 4g .. 4g + 3 of each 16-row block; the dK/dV stage: row
+    // l & 15 of each 16-key block, columns 4g ..
+    const int g16 = lane >> 4, i16 = lane & 15;
+    const int hs_rco = 16 * g16, hs_rvo = 4 * lane;
     const int hs_rcw = (wave < 2 ? 256 * wave : 512) + 4 * lane;
-    const int hs_oak = ((wave * 64 + r) * OST + 4 * h) * 4, hs_oav = hs_oak + 256 * OST * 4;
+    const int hs_oak = ((wave * 64 + i16) * OST + 4 * g16) * 4, hs_oav = hs_oak + 256 * OST * 4;
     const __amdgpu_buffer_rsrc_t hs_rsq = qs.rs, hs_rsd = ds.rs;
     // the row-constant stream of this wave: LSE (wave 0), Δ (wave 1), nothing (num_records 0)
     const __amdgpu_buffer_rsrc_t hs_rsc = head_rsrc(wave == 1 ? Delta + rbase : LSE + rbase, wave < 2 ? S : 0, 1);
@@ -1436,7 +1422,7 @@ fa2_bwd_dq_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, 
                       const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
                       float* __restrict__ dQ, int S, const float* __restrict__ O) {
     __shared__ __attribute__((aligned(16))) char lds[DqLds<D, NW, DELTA, NKB, KS>::BYTES];
-    dq_body<D, NW, DELTA, NKB, M16, KS, KS == 1 && D == 64 ? FA2_IGLP_DQ : -1>(
+    dq_body<D, NW, DELTA, NKB, M16, KS, KS == 1 && D == 64 ? kIglpDq : -1>(
         lds, xcd_remap(blockIdx.x, gridDim.x), Q, K, V, dO, LSE, Delta, dQ, S, O);
 }
 
@@ -1463,10 +1449,10 @@ fa2_bwd_fused_f16_kernel(const float* __restrict__ Q, const float* __restrict__ 
     const int b = blockIdx.x;
     if (b < ndk)
         // the dK/dV role with unsplit queries takes the standalone kernel's strategy
-        dkdv_body<D, NW, 1, true, QS, DEL, QS == 1 && D == 64 ? FA2_IGLP_DKDV : FA2_IGLP_FUSED>(
+        dkdv_body<D, NW, 1, true, QS, DEL, QS == 1 && D == 64 ? kIglpDkdv : kIglpFused>(
             lds, xcd_remap(b, ndk), Q, K, V, dO, LSE, Delta, dK, dV, S, O);
     else
-        dq_body<D, NW, DEL, NKB, true, KS, FA2_IGLP_FUSED>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
+        dq_body<D, NW, DEL, NKB, true, KS, kIglpFused>(lds, xcd_remap(b - ndk, gridDim.x - ndk), Q, K, V, dO, LSE,
                                                            Delta, dQ, S, O);
 }
 
@@ -1712,14 +1698,17 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     // 4-tile staging registers spill).  Measured (B2_H8_D64, r01): S = 512 16.1 -> 12.1
     // us, 1024 29.1 -> 20.8, 2048 53.7 -> 44.3.
     int qs = tune_knob("DKDV_QS", 0);
+    // a forced DKDV_HS the plan cannot take (D, or other plan knobs) is an error, never a
+    // silent launch of another kernel
+    if (tune_knob("DKDV_HS", -1) == 1 && (D != 64 || nw || qs)) return hipErrorInvalidValue;
     if constexpr (D == 64) {
-        // hand-scheduled kernel (r05): whole 64-query steps, and a grid of at least one
-        // 256-key workgroup per CU.  DKDV_HS (tests and tools): 1 forces it (an error where
-        // it cannot serve), 0 disables it.  Default off: alone it beats the 8-wave
-        // 16x16x32 kernel (C3 134.2 vs 134.7 us, B16_H16_S2048 529.3 vs 552.9; r05,
-        // profiles/r05/dkhs/), but the fwd + bwd step with it is 0.6-2.2 % slower
-        // (C3 dO = ones 0.2952 vs 0.2905 ms; profiles/r05/dkhs_ones/)
-        const int hs = tune_knob("DKDV_HS", 0);
+        // hand-scheduled kernel: whole 64-query steps, and a grid of at least one 256-key
+        // workgroup per CU.  DKDV_HS (tests and tools): 1 forces it (an error where it
+        // cannot serve), 0 disables it.  r06, on 16x16x32 (the r05 32x32x16 form lost inside
+        // the step): in one process against the 8-wave kernel, dK/dV -3.1 .. -4.5 % and the
+        // fwd + bwd step -1.5 .. -2.1 % at C3, B2_H8_S4096 and B16_H16_S2048, dO = ones and
+        // N(0,1) (profiles/r06/dkhs16/)
+        const int hs = tune_knob("DKDV_HS", -1);
         const bool fits = S % 64 == 0 && S >= 128;
         if (hs == 1 && !fits) return hipErrorInvalidValue;
         const long hgrid = (long)bh * ((S + 255) / 256);
@@ -1780,6 +1769,7 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     // tiles with the 4-tile staging registers spill).  Measured (B2_H8_D64 dQ + Δ,
     // r01): S = 512 17.0 -> 11.4 us, 1024 29.5 -> 15.7, 2048 41.9 -> 36.7.
     int ksp = tune_knob("DQ_KS", 0);
+    if (tune_knob("DQ_HS", -1) == 1 && (D != 64 || nw || ksp)) return hipErrorInvalidValue;
     if constexpr (D == 64) {
         // hand-scheduled kernel (r05): whole 64-key tiles, and a grid of at least one
         // 256-row workgroup per CU.  DQ_HS (tests and tools): 1 forces it (an error where it
@@ -1959,6 +1949,8 @@ hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* 
     int fused = tune_knob("BWD_FUSED", -1);
     if (fused < 0) fused = bh > 0 && S > 0 && auto_waves((long)bh * ((S + 31) / 32), 8) < 8;
     if (D <= 64 && bh > 0 && S > 0 && fused == 1) {
+        // the fused launch has no hand-scheduled roles: forcing one is an error
+        if (tune_knob("DQ_HS", -1) == 1 || tune_knob("DKDV_HS", -1) == 1) return hipErrorInvalidValue;
         // Δ inside the fused launch below 4 blocks of 32 rows per CU (override
         // BWD_FUSED_DELTA; 0 = the separate Δ kernel first).  Measured (B2_H8_D64 fwd +
         // bwd, r02): S = 512 29.9 -> 26.7 us, S = 1024 45.0 -> 40.8; at S = 2048 (4

@@ -278,9 +278,7 @@ struct FwdState {
 // D = 128; -1 = the default scheduler.  r03 in-process A/Bs (`profiles/r03/ab/figlp/`):
 // strategy 0 took C4 (B8_H16_S4096_D128) 1.2-1.5 % faster in two runs, D = 128 at S = 2048
 // +-0; at D = 64 every strategy (0-3) lost 5 % at C3, so D = 64 keeps the default.
-#ifndef FA2_FWD_IGLP
-#define FA2_FWD_IGLP 0
-#endif
+constexpr int kFwdIglp = 0;
 
 // -m as one opaque 16-register tuple: without the empty asm the compiler
 // rematerialises the splat with 16 v_mov before every QK^T chain.
@@ -297,10 +295,7 @@ __device__ __forceinline__ f32x16 splat16(float x) {
 template <int D, int MQ, int NKB = 2, bool SEED = true>
 __device__ __forceinline__ void fwd_qk(f32x16 (&s)[MQ][NKB], const FwdState<D> (&st)[MQ], const _Float16* Ks,
                                        const FragOffsets<D>& fo) {
-    if constexpr (D == 128 && FA2_FWD_IGLP >= 0) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP);
-#ifdef FA2_FWD_IGLP_QK64
-    if constexpr (D == 64) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP_QK64);
-#endif
+    if constexpr (D == 128) __builtin_amdgcn_iglp_opt(kFwdIglp);
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
         const f16x8 a0 = fo.rowop(Ks, kb * 32, 0);
@@ -377,10 +372,7 @@ __device__ __forceinline__ void fwd_softmax_pv(FwdState<D> (&st)[MQ], f32x16 (&s
     // audit: 29 v_mov per 64-key tile at D = 64; 32 v_mov_b64 + 5 v_mov_b32 per 32-key
     // tile at D = 128); joined after it, the merged values are MFMA results.
     auto accumulate = [&]() {
-        if constexpr (D == 128 && FA2_FWD_IGLP >= 0) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP);
-#ifdef FA2_FWD_IGLP_PV64
-        if constexpr (D == 64) __builtin_amdgcn_iglp_opt(FA2_FWD_IGLP_PV64);
-#endif
+        if constexpr (D == 128) __builtin_amdgcn_iglp_opt(kFwdIglp);
 #pragma unroll
         for (int g = 0; g < MQ; ++g)
 #pragma unroll
@@ -811,10 +803,7 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
 // checked against 2^13 (fp16 range of P), and a block where any was out of range (or
 // NaN) is recomputed by the robust compiler-scheduled loop below.
 }  // namespace fa2f16
-#ifndef FA2_HS_INC
-#define FA2_HS_INC "fa2_fwd_hs.inc"  // (timing-only ablation builds name another, tools/r05_hs_abl.sh)
-#endif
-#include FA2_HS_INC
+#include "fa2_fwd_hs.inc"
 namespace fa2f16 {
 
 template <int D>
@@ -887,7 +876,10 @@ fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, cons
 #endif
     }
 
-    if (!__syncthreads_or(hs_flag != 0)) {
+    // hs_flag is a scalar (wave-uniform): this wave saw a half-row sum out of range
+    const bool wave_bad = hs_flag != 0;
+    const bool any_bad = __syncthreads_or(wave_bad);
+    if (!wave_bad) {
         // O rows [wave*64 + c*32 + q][OST] (unnormalised) are in the stage; l is per lane
         // half: the xor-32 sum is the row's total
         const float lt0 = xor32_sum(hs_l0), lt1 = xor32_sum(hs_l1);
@@ -908,30 +900,38 @@ fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, cons
             const f32x4 v = *reinterpret_cast<const f32x4*>(os + row * OST + c4) * invl[row];
             if (qrow0 + row < S) *reinterpret_cast<f32x4*>(O + base + (long)(qrow0 + row) * D + c4) = v;
         }
-        return;
     }
-    // Robust path (a late score spike somewhere in the block): both chains of every wave
-    // recomputed with the rescaling loop (first tile sets m, later tiles move it when
-    // their sums leave range), one chain at a time.
-#pragma unroll 1
-    for (int c = 0; c < 2; ++c) {
-        FwdState<D> st[1];
-        const int q = qrow0 + wave * 64 + c * 32 + r;
+    if (!any_bad) return;
+    // Robust path (a late score spike in some wave's rows): only the flagged waves
+    // recompute, both chains in ONE pass over the head's K/V with the rescaling loop
+    // (first tile sets m, later tiles move it when their sums leave range); the other
+    // waves have stored their rows above and only help stage the tiles.  The barrier
+    // keeps the restaging from overwriting an O stage another wave still reads.
+    __syncthreads();
+    FwdState<D> st[2];
+    const int q = qrow0 + wave * 64 + r;
+    if (wave_bad) {
         fwd_init<D>(st[0], Q, base, q, S, h);
-        const int ntiles = (S + KT - 1) / KT;
+        fwd_init<D>(st[1], Q, base, q + 32, S, h);
+    }
+    const int ntiles = (S + KT - 1) / KT;
 #pragma unroll 1
-        for (int j = 0; j < ntiles; ++j) {
-            ks.load(j * KT);
-            vs.load(j * KT);
-            __syncthreads();
-            ks.store(smem, 1.f, tid);
-            vs.store(smem + TB, 1.f, tid);
-            __syncthreads();
-            f32x16 sacc[1][2];
-            fwd_qk<D, 1, 2, true>(sacc, st, smem, fo);
-            fwd_softmax_pv<D, 1, false, 2, true>(st, sacc, smem + TB, fo, j * KT, S, h, j == 0);
+    for (int j = 0; j < ntiles; ++j) {
+        ks.load(j * KT);
+        vs.load(j * KT);
+        if (j) __syncthreads();  // the previous tile's reads are done
+        ks.store(smem, 1.f, tid);
+        vs.store(smem + TB, 1.f, tid);
+        __syncthreads();
+        if (wave_bad) {
+            f32x16 sacc[2][2];
+            fwd_qk<D, 2, 2, true>(sacc, st, smem, fo);
+            fwd_softmax_pv<D, 2, false, 2, true>(st, sacc, smem + TB, fo, j * KT, S, h, j == 0);
         }
+    }
+    if (wave_bad) {
         fwd_store<D>(st[0], O, LSE, base, (long)bh * S, q, S, h);
+        fwd_store<D>(st[1], O, LSE, base, (long)bh * S, q + 32, S, h);
     }
 }
 #endif  // CUPY_INLINE_COMPILE
@@ -1047,10 +1047,13 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
         // per MFMA cycle)
         const int hs = tune_knob("FWD_HS", -1);
         const bool fits = S % 64 == 0 && S >= 128;
-        if (hs == 1 && !fits) return hipErrorInvalidValue;
         const bool forced_other = tune_knob("FWD_WAVES", 0) || tune_knob("FWD_KS", 0) || tune_knob("FWD_NKB", 0);
+        // a forced FWD_HS the plan cannot take (shape, or other plan knobs) is an error
+        if (hs == 1 && (!fits || forced_other)) return hipErrorInvalidValue;
         if (fits && (hs == 1 || (hs < 0 && !forced_other && (long)bh * ((S + 255) / 256) >= cu_count())))
             return fwd_hs_launch<D>(q, k, v, o, lse, bh, S, stream);
+    } else {
+        if (tune_knob("FWD_HS", -1) == 1) return hipErrorInvalidValue;  // no hand-scheduled kernel at this D
     }
     // 8 waves (2 per SIMD) where the registers allow it; D = 128 runs 4 waves of
     // ~400 VGPRs (8 would spill and exceed the LDS budget with the Q stages)
@@ -1067,6 +1070,7 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
     int ks = tune_knob("FWD_KS", 0);
     // FWD_NKB (0 = auto): 32-key (1) or 64-key (2) tiles of a key-split plan
     int nkb = tune_knob("FWD_NKB", 0);
+    if (nkb < 0 || nkb > 2) return hipErrorInvalidValue;
     if (ks == 0 && nw == 0 && D <= 64 && units < 8L * cu_count()) {
         // D <= 64 on fewer than 8 blocks of 32 rows per CU: the fewest query rows per
         // workgroup whose grid still runs in ONE round of workgroups (one per CU; every
@@ -1100,9 +1104,9 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
         // MFMAs per barrier of the 32-key tiles): B2_H8_S2048 fwd 29.6 -> 25.4 us, step
         // 99.1 -> 95.7; B4_H8_S1024 fwd 18.1 -> 15.8; S = 1500 22.3 -> 19.1
         // (profiles/r04/nkb/).  KS = 4 keeps 32-key tiles at 8 waves (64-key tiles spill).
-        if (ks == 2 && nw == 8 && nkb != 1) return fwd_f16_launch<D, 8, 2, 2>(q, k, v, o, lse, bh, S, stream, 0);
-        if (ks == 2 && nw == 8) return fwd_f16_launch<D, 8, 2, 1>(q, k, v, o, lse, bh, S, stream, 0);
-        if (ks == 4 && nw == 4 && nkb == 2) return fwd_f16_launch<D, 4, 4, 2>(q, k, v, o, lse, bh, S, stream, 0);
+        if (ks == 2 && nw == 8 && nkb != 1) return fwd_f16_launch<D, 8, 2, 2>(q, k, v, o, lse, bh, S, stream, nkb);
+        if (ks == 2 && nw == 8) return fwd_f16_launch<D, 8, 2, 1>(q, k, v, o, lse, bh, S, stream, nkb);
+        if (ks == 4 && nw == 4 && nkb == 2) return fwd_f16_launch<D, 4, 4, 2>(q, k, v, o, lse, bh, S, stream, nkb);
         if (ks == 4 && nw == 8) return fwd_f16_launch<D, 8, 4>(q, k, v, o, lse, bh, S, stream, nkb);
         if (ks == 4 && nw == 4) return fwd_f16_launch<D, 4, 4>(q, k, v, o, lse, bh, S, stream, nkb);
         if (ks == 2 && nw == 4) return fwd_f16_launch<D, 4, 2>(q, k, v, o, lse, bh, S, stream, nkb);

@@ -2,9 +2,8 @@
 
 fa2_bwd_dq_hs_kernel<64> (generated asm loop, gen/gen_bwd_dq.py) computes dQ (and Δ, when
 it gets O) and fa2_bwd_dkdv_hs_kernel<64> (gen/gen_bwd_dkdv.py) dK and dV, for D = 64 on
-whole 64-row tiles.  The dQ kernel is the default launch wherever its grid holds at least
-one 256-row workgroup per CU (C3, C5, the S = 4096 sweep point); the dK/dV kernel is
-opt-in (DKDV_HS = 1: alone it beats the 8-wave kernel, inside the step it loses).  DQ_HS = 1 /
+whole 64-row tiles.  Both are the default launches wherever their grid holds at least
+one 256-row workgroup per CU (C3, C5, the S = 4096 sweep point).  DQ_HS = 1 /
 DKDV_HS = 1 force them onto the small shapes here: one and several 256-row blocks per head, a last block
 with rows past S, every exit of the dK/dV loop's three-step unroll, N(0,1) inputs and
 gradients, both tile types, Δ fused (O given) and Δ supplied.  Tolerances are the north star's (1e-2 fp16, 2e-2 bf16, gradients scaled
@@ -111,14 +110,14 @@ def test_hs_dkdv_entry_point():
 
 
 def test_hs_dkdv_deterministic_and_default():
-    """bitwise repeatable (the hand-scheduled dK/dV is opt-in: DKDV_HS = 1)"""
+    """bitwise repeatable; at C3's grid the default dK/dV launch is the hand-scheduled one"""
     B, H, S, D = 4, 16, 2048, 64
     q, k, v = fo.harness_inputs(B, H, S, D, seed=4)
     do = np.random.RandomState(10).randn(B, H, S, D).astype(np.float32)
     tq, tk, tv, tdo = cuda(q, k, v, do)
     o, lse = fa2amd.forward(tq, tk, tv, "fp16")
     res = []
-    for hs in (1, 1, 1, 0):
+    for hs in (-1, 1, 1, 0):
         fa2amd.tune_set("DKDV_HS", hs)
         dq, dk, dv = fa2amd.backward(tq, tk, tv, o, tdo, lse, "fp16")
         torch.cuda.synchronize()
@@ -156,6 +155,40 @@ def test_hs_bwd_forced_on_unserved_shape_is_an_error(shape, knob):
     fa2amd.tune_set(knob, 1)
     fa2amd.tune_set("BWD_FUSED", 0)
     (q, k, v, do, o, lse), _ = _case(shape)
+    tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
+    with pytest.raises(fa2amd.FA2Error):
+        fa2amd.backward(tq, tk, tv, to, tdo, tl, "fp16")
+
+
+@pytest.mark.parametrize("knob", ["DQ_HS", "DKDV_HS"])
+def test_hs_bwd_forced_onto_the_fused_plan_is_an_error(knob):
+    """a small grid picks the fused one-launch backward, which has no hand-scheduled
+    roles: forcing DQ_HS / DKDV_HS there (without BWD_FUSED = 0) is an error"""
+    fa2amd.tune_set(knob, 1)
+    (q, k, v, do, o, lse), _ = _case((1, 2, 256, 64))
+    tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
+    with pytest.raises(fa2amd.FA2Error):
+        fa2amd.backward(tq, tk, tv, to, tdo, tl, "fp16")
+
+
+@pytest.mark.parametrize("knobs", [{"DQ_HS": 1, "DQ_WAVES": 8}, {"DQ_HS": 1, "DQ_KS": 2},
+                                   {"DKDV_HS": 1, "DKDV_WAVES": 8}, {"DKDV_HS": 1, "DKDV_QS": 2}],
+                         ids=lambda k: "_".join(f"{a}{b}" for a, b in sorted(k.items())))
+def test_hs_bwd_forced_with_other_plan_knobs_is_an_error(knobs):
+    for key, val in knobs.items():
+        fa2amd.tune_set(key, val)
+    fa2amd.tune_set("BWD_FUSED", 0)
+    (q, k, v, do, o, lse), _ = _case((1, 2, 256, 64))
+    tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
+    with pytest.raises(fa2amd.FA2Error):
+        fa2amd.backward(tq, tk, tv, to, tdo, tl, "fp16")
+
+
+@pytest.mark.parametrize("knob", ["DQ_HS", "DKDV_HS"])
+def test_hs_bwd_forced_at_other_head_dims_is_an_error(knob):
+    fa2amd.tune_set(knob, 1)
+    fa2amd.tune_set("BWD_FUSED", 0)
+    (q, k, v, do, o, lse), _ = _case((1, 2, 256, 32))
     tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
     with pytest.raises(fa2amd.FA2Error):
         fa2amd.backward(tq, tk, tv, to, tdo, tl, "fp16")

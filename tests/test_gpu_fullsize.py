@@ -117,6 +117,36 @@ def test_c3_every_head_harness_rule(c3_oracle, precision):
     assert_identities(q, v, ones, o, dk, dv)
 
 
+def randn_do(B, H, S, D):
+    """the bench's realistic upstream gradient (bench.py extra_configs.c3_dO_randn):
+    dO ~ N(0, 1) from torch.Generator seed 43"""
+    return torch.randn(B, H, S, D, generator=torch.Generator().manual_seed(43)).numpy()
+
+
+@pytest.fixture(scope="module")
+def c3_oracle_randn(c3_oracle):
+    q, k, v, _, eo, el, _ = c3_oracle
+    do = randn_do(4, 16, 2048, 64)
+    edq, edk, edv = c_oracle.backward(q, k, v, eo, do, el, NT)
+    return do, (edq, edk, edv)
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_c3_every_head_gaussian_gradient(c3_oracle, c3_oracle_randn, precision):
+    """C3 fwd+bwd on all 64 heads with dO ~ N(0, 1) (seed 43, the bench's c3_dO_randn
+    input) instead of the harness's ones: |dQ| reaches O(1) here (with dO = ones it stays
+    below 0.013), so the gradients are held to the tolerance scaled by max(1, max|ref|),
+    per tensor, as test_gpu_parity.py does for its N(0, 1) gradients."""
+    q, k, v, _, eo, el, _ = c3_oracle
+    do, exp = c3_oracle_randn
+    o, lse, dq, dk, dv = gpu_fwd_bwd(q, k, v, do, precision)
+    assert maxerr(o, eo) < TOL[precision] and maxerr(lse, el) < TOL[precision]
+    for got, e in zip((dq, dk, dv), exp):
+        assert np.isfinite(got).all()
+        assert maxerr(got, e) < TOL[precision] * max(1.0, float(np.abs(e).max()))
+    assert_identities(q, v, do, o, dk, dv)
+
+
 # ---------------------------------------------------------------------------
 # C4: the long-sequence D = 128 forward, every head
 # ---------------------------------------------------------------------------
@@ -214,6 +244,23 @@ def test_c5_host_api_8way_split(c5_data):
     o1, l1, dq1, dk1, dv1 = gpu_fwd_bwd(heads(q, sl), heads(k, sl), heads(v, sl), heads(ones, sl), "fp16")
     for a, b in ((o, o1), (lse, l1), (dq, dq1), (dk, dk1), (dv, dv1)):
         assert np.array_equal(heads(a, sl), b)
+
+
+def test_c5_sample_heads_gaussian_gradient(c5_data):
+    """C5 (one GPU, all 1024 heads computed) with dO ~ N(0, 1) (seed 43): the 32 spread
+    sample heads (both ends and every 8-way shard's first and last head) against the
+    oracle, gradients scaled by max(1, max|ref|); identities on every head."""
+    q, k, v, _, _ = c5_data
+    do = randn_do(*C5)
+    o, lse, dq, dk, dv = gpu_fwd_bwd(q, k, v, do, "fp16")
+    idx = [h for h in C5_SAMPLE if h not in set(C5_SHARD)]
+    qs, ks, vs, dos = (heads(x, idx) for x in (q, k, v, do))
+    eo, el = c_oracle.forward(qs, ks, vs, NT)
+    assert maxerr(heads(o, idx), eo) < TOL["fp16"] and maxerr(heads(lse, idx), el) < TOL["fp16"]
+    for got, e in zip((dq, dk, dv), c_oracle.backward(qs, ks, vs, eo, dos, el, NT)):
+        assert np.isfinite(got).all()
+        assert maxerr(heads(got, idx), e) < TOL["fp16"] * max(1.0, float(np.abs(e).max()))
+    assert_identities(q, v, do, o, dk, dv)
 
 
 @pytest.mark.parametrize("chunks", [0, 2, 3])

@@ -129,11 +129,37 @@ def test_hs_is_default_on_full_grids():
 
 @pytest.mark.parametrize("shape", [(1, 1, 100, 64), (1, 1, 64, 64), (1, 1, 256, 32)])
 def test_hs_forced_on_unserved_shape_is_an_error(shape):
+    """FWD_HS = 1 where the kernel cannot serve (ragged S, S < 128, D = 32, which has no
+    hand-scheduled kernel) is an error, never a silent launch of another plan"""
     fa2amd.tune_set("FWD_HS", 1)
     q, k, v = cuda(*fo.harness_inputs(*shape))
-    if shape[3] == 32:  # D = 32 has no hand-scheduled kernel: the knob does not apply
-        fa2amd.forward(q, k, v, "fp16")
-        torch.cuda.synchronize()
-        return
     with pytest.raises(fa2amd.FA2Error):
         fa2amd.forward(q, k, v, "fp16")
+
+
+@pytest.mark.parametrize("other", [("FWD_WAVES", 8), ("FWD_KS", 2), ("FWD_NKB", 2)])
+def test_hs_forced_with_other_plan_knobs_is_an_error(other):
+    fa2amd.tune_set("FWD_HS", 1)
+    fa2amd.tune_set(*other)
+    q, k, v = cuda(*fo.harness_inputs(1, 2, 512, 64))
+    with pytest.raises(fa2amd.FA2Error):
+        fa2amd.forward(q, k, v, "fp16")
+
+
+@pytest.mark.parametrize("D", [64, 128])
+def test_hs_forward_restart_some_waves(D):
+    """A late key that spikes the scores of ONE wave's 64 rows only (query rows 64..127 of
+    the first block get a large first component, the late key too: +15 nats, past the
+    2^13 tile-sum guard, for those rows only): that wave recomputes with the rescaling
+    loop, the other waves keep their loop results; every row matches the oracle.  (fp16
+    tiles: at scores of ~20 nats bf16's 8-bit significand alone is worth ~0.03 in LSE)"""
+    B, H, S = 1, 2, 1024
+    q, k, v = fo.harness_inputs(B, H, S, D, seed=13)
+    q, k = q.copy(), k.copy()
+    q[:, :, 64:128, 0] = 10.0
+    k[:, :, 900, 0] = 12.0 * np.sqrt(D / 64.0)
+    eo, el = fo.attention_forward(q, k, v)
+    o, lse = run(q, k, v, "fp16", hs=1)
+    assert np.isfinite(o).all() and np.isfinite(lse).all()
+    assert maxerr(o, eo) < TOL["fp16"]
+    assert maxerr(lse, el) < TOL["fp16"]

@@ -42,7 +42,7 @@ def test_dq_loop(S, block, bf16):
     sim("--kernel", "dq", "--D", "64", "--S", str(S), "--block", str(block), *(["--bf16"] if bf16 else []))
 
 
-@pytest.mark.parametrize("S,block,bf16", [(192, 0, False), (256, 0, False), (320, 0, True), (384, 0, False),
+@pytest.mark.parametrize("S,block,bf16", [(128, 0, False), (192, 0, False), (256, 0, False), (320, 0, True), (384, 0, False),
                                           (512, 1, False)])
 def test_dkdv_loop(S, block, bf16):
     sim("--kernel", "dkdv", "--D", "64", "--S", str(S), "--block", str(block), *(["--bf16"] if bf16 else []))

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Phase stamps of the hand-scheduled forward loop (a 'stamps' timing build:
-tools/r05_hs_abl.sh fw_stamps:fwd:stamps).  The build's asm records s_memtime (shader
+tools/abl_build.sh fw_stamps:fwd:stamps).  The build's asm records s_memtime (shader
 clock) into lane k % 64 of one VGPR at every stamp k and leaves the 64 lanes (low 24 bits,
 as floats) in O columns 2 / 6 of each wave's rows, the stamp count in columns 3 / 7.
 Stamps: 0 entry, 1 loop entry, then per tile P1 start, P2 start, P3 start, barrier
