@@ -144,7 +144,8 @@ def test_c3_every_head_gaussian_gradient(c3_oracle, c3_oracle_randn, precision):
     for got, e in zip((dq, dk, dv), exp):
         assert np.isfinite(got).all()
         assert maxerr(got, e) < TOL[precision] * max(1.0, float(np.abs(e).max()))
-    assert_identities(q, v, do, o, dk, dv)
+    # the column sums of dV are O(100) here: bf16's 8-bit significand is worth ~0.3 on them
+    assert_identities(q, v, do, o, dk, dv, atol=0.05 if precision == "fp16" else 0.5)
 
 
 # ---------------------------------------------------------------------------
