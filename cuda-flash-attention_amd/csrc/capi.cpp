@@ -65,7 +65,7 @@ std::atomic<int> g_tune_n{0};
 // the launch-plan overrides the launchers read (fa2_tune_set rejects other names,
 // so a misspelt knob cannot silently leave an A/B on the default plan)
 const char* const kKnobs[] = {"FWD_HS",   "FWD_WAVES", "FWD_KS",          "FWD_NKB", "DKDV_WAVES", "DKDV_QS",
-                              "DKDV_HS",  "DQ_WAVES",  "DQ_KS",           "DQ_HS",   "BWD_FUSED",  "BWD_FUSED_DELTA", "BWD_H16",
+                              "DKDV_HS",  "DQ_WAVES",  "DQ_KS",           "DQ_HS",   "BWD_FUSED",  "BWD_FUSED_DELTA",
                               "BWD_FQS",  "BWD_FKS",   "BWD_FNW",         "HOST_SHARDS_ON_DEVICE0",    "HOST_CHUNKS"};
 bool known_knob(const char* k) {
     for (const char* n : kKnobs)

@@ -59,15 +59,14 @@ KEYS = 256  # keys per workgroup
 
 
 class Cfg:
-    def __init__(self, D, bf16, src16=False):
+    def __init__(self, D, bf16):
         assert D == 64
-        # src16: Q and dO stream from 16-bit copies (the dQ kernel writes them inside
-        # fa2_backward): one 16-B load per 8-element chunk straight into LDS, no conversion
-        self.D, self.bf16, self.src16 = D, bf16, src16
+        self.D, self.bf16 = D, bf16
         self.KS, self.NMD, self.NB, self.CPT = D // 32, D // 16, 4, D // 32
         self.exp_per_gap = 1
         # per-gap filler budget floor, 16-cycle MFMAs: 8 (r06 A/B, profiles/r06/dksched/: step -0.2 .. -0.7 %
-        # against 12 in all six C3 / B2_H8_S4096 / B16_H16_S2048 cases, 16 +0.1 .. +1.2 %)
+        # against 12 in all six C3 / B2_H8_S4096 / B16_H16_S2048 cases, 16 +0.1 .. +1.2 %; 6, 4 and
+        # 2 v_exp per gap within +-0.3 %, profiles/r06/sched2/)
         self.min_cap = 8
         self.TBB = QT * D * 2  # one 16-bit [64][D] tile
         # a slot: Q, dO tiles + row constants -LSE*log2e, -Delta (and a 256-B sink that waves
@@ -245,14 +244,13 @@ def staging_loads(cfg):
     for tensor, rs in ((0, "%[rsq]"), (1, "%[rsd]")):
         for cc in range(cfg.CPT):
             base = cfg.stg(tensor, cc)
-            for h in range(1 if cfg.src16 else 2):
+            for h in range(2):
                 off = f" offset:{16 * h}" if h else ""
                 out.append(Ins(f"buffer_load_dwordx4 {rtxt('v', base + 4 * h, 4)}, %[vo{cc}], {rs}, %[goff] offen{off}",
                                "vmem", R(["s:goff"]), rng("v", base + 4 * h, 4)))
     out.append(Ins(f"buffer_load_dword v{cfg.RCV}, %[rvo], %[rsc], %[roff] offen", "vmem", R(["s:roff"]),
                    [f"v{cfg.RCV}"]))
-    out.append(Ins(f"s_add_u32 %[goff], %[goff], {QT * cfg.D * (2 if cfg.src16 else 4)}", "salu", R(["s:goff"]),
-                   ["s:goff", "scc"]))
+    out.append(Ins(f"s_add_u32 %[goff], %[goff], {QT * cfg.D * 4}", "salu", R(["s:goff"]), ["s:goff", "scc"]))
     out.append(Ins(f"s_add_u32 %[roff], %[roff], {QT * 4}", "salu", R(["s:roff"]), ["s:roff", "scc"]))
     return tagged("stg", out)
 
@@ -263,7 +261,7 @@ def staging_convert(cfg, slot):
     for tensor in range(2):
         for cc in range(cfg.CPT):
             base = cfg.stg(tensor, cc)
-            for ii in range(0 if cfg.src16 else 4):
+            for ii in range(4):
                 d, a, b = base + ii, base + 2 * ii, base + 2 * ii + 1
                 out.append(valu(f"{cfg.cvt} v{d}, v{a}, v{b}", [f"v{a}", f"v{b}"], [f"v{d}"]))
             off = slot * cfg.SLOT + tensor * cfg.TBB + cc * step * cfg.D * 2
@@ -368,8 +366,7 @@ def epilogue(cfg, last_slot_expr):
 
 
 def build(cfg):
-    log = [f"dK/dV D={cfg.D} {'bf16' if cfg.bf16 else 'fp16'}{' (16-bit Q, dO)' if cfg.src16 else ''}: "
-           f"{cfg.nvgpr} VGPRs + {cfg.nagpr} AGPRs in asm, "
+    log = [f"dK/dV D={cfg.D} {'bf16' if cfg.bf16 else 'fp16'}: {cfg.nvgpr} VGPRs + {cfg.nagpr} AGPRs in asm, "
            f"LDS {cfg.lds_bytes} B"]
     pro = prologue(cfg)
     bodies = [ablate(body(cfg, j3, log)) for j3 in (1, 2, 0)]
@@ -444,11 +441,11 @@ def emit():
            "// Hand-scheduled dK/dV loop of fa2_bwd_dkdv_hs_kernel<D> (f-attn2-backward_f16.cu).",
            "#pragma once", ""]
     logs = []
-    for bf16, src16 in ((False, False), (True, False), (False, True), (True, True)):
-        cfg = Cfg(64, bf16, src16)
+    for bf16 in (False, True):
+        cfg = Cfg(64, bf16)
         lines, log = build(cfg)
         logs += log
-        out.append(f"#define FA2_DK_ASM_D64_{'BF16' if bf16 else 'F16'}{'_S16' if src16 else ''} \\")
+        out.append(f"#define FA2_DK_ASM_D64_{'BF16' if bf16 else 'F16'} \\")
         out += [f'    "{ln}\\n\\t" \\' for ln in lines]
         out.append('    ""')
         out.append("")

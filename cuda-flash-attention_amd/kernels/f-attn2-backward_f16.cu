@@ -25,8 +25,6 @@
 //
 // Self-contained device code (hiprtc-compilable with -DCUPY_INLINE_COMPILE, C++14).
 #ifndef CUPY_INLINE_COMPILE
-#include <type_traits>
-
 #include "f-attn2.cuh"
 #endif
 
@@ -226,51 +224,6 @@ struct TileStager {
         for (int c = 0; c < CPT; ++c)
             if (EXACT || tid + c * NT < CHUNKS)
                 *reinterpret_cast<f16x8*>(tile + loff[c]) = to_f16x8(r[c][0], r[c][1], scale);
-    }
-};
-
-// 16-bit copies of a staged block (the dQ kernel's hand-off to the dK/dV kernel inside
-// fa2_backward): the stager's fp32 rows, rounded to the tile type exactly as store() does
-// (scale 1), written as whole 16-B chunks at the same element offsets; rows >= S skipped.
-template <int D, int ROWS, int NT>
-__device__ __forceinline__ void store_tile16(const TileStager<D, ROWS, NT>& st, _Float16* __restrict__ head16, int row0,
-                                             int S, int tid) {
-    using TS = TileStager<D, ROWS, NT>;
-#pragma unroll
-    for (int c = 0; c < TS::CPT; ++c) {
-        const int x = tid + c * NT;
-        if ((TS::EXACT || x < TS::CHUNKS) && row0 + x / TS::CPR < S)
-            *reinterpret_cast<f16x8*>(head16 + (long)row0 * D + st.voff[c] / 4) = to_f16x8(st.r[c][0], st.r[c][1], 1.f);
-    }
-}
-// Register-staged loader of a 16-bit [S][D] head (the copies above): one 16-B load per
-// 8-element chunk, stored to the swizzled LDS tile unchanged; rows >= S read as zeros.
-template <int D, int ROWS, int NT>
-struct TileStager16 {
-    static constexpr int CPR = D / 8, CHUNKS = ROWS * CPR, CPT = (CHUNKS + NT - 1) / NT;
-    static constexpr bool EXACT = CHUNKS % NT == 0;
-    f32x4 r[CPT];
-    int voff[CPT], loff[CPT];
-    __amdgpu_buffer_rsrc_t rs;
-    __device__ __forceinline__ void init(const _Float16* head_base, int S, int tid) {
-        // a 16-bit head is S * D / 2 fp32 words: head_rsrc's byte count
-        rs = head_rsrc(reinterpret_cast<const float*>(head_base), S, D / 2);
-#pragma unroll
-        for (int c = 0; c < CPT; ++c) {
-            const int x = tid + c * NT;
-            const int row = x / CPR, ch = x % CPR;
-            voff[c] = (EXACT || x < CHUNKS) ? (row * D + ch * 8) * 2 : 0x7ffffff0;
-            loff[c] = row * D + ((ch ^ Swz<D>::f(row)) << 3);
-        }
-    }
-    __device__ __forceinline__ void load(int row0) {
-#pragma unroll
-        for (int c = 0; c < CPT; ++c) r[c] = buf_load4(rs, voff[c], row0 * D * 2);
-    }
-    __device__ __forceinline__ void store(_Float16* tile, int tid) const {
-#pragma unroll
-        for (int c = 0; c < CPT; ++c)
-            if (EXACT || tid + c * NT < CHUNKS) *reinterpret_cast<f32x4*>(tile + loff[c]) = r[c];
     }
 };
 
@@ -1248,8 +1201,7 @@ template <int D>
 __global__ void __launch_bounds__(256, 1)
 fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                      const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
-                     float* __restrict__ dQ, int S, const float* __restrict__ O, _Float16* __restrict__ Q16,
-                     _Float16* __restrict__ dO16) {
+                     float* __restrict__ dQ, int S, const float* __restrict__ O) {
     static_assert(D == 64, "hand-scheduled dQ: D = 64");
     constexpr int KT = 64, TB = KT * D, OST = D + 4;
     __shared__ __attribute__((aligned(16))) _Float16 smem[FA2_DQ_LDS_D64 / 2];
@@ -1270,7 +1222,6 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
         qst.init(Q + base, S, tid);
         qst.load(qrow0);
         qst.store(smem + 4 * TB, FA2B_LOG2E / __builtin_sqrtf((float)D), tid);
-        if (Q16) store_tile16(qst, Q16 + base, qrow0, S, tid);  // unscaled: the dK/dV kernel's Q
     }
     {
         TileStager<D, 256, 256> dst;
@@ -1283,7 +1234,6 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
             delta_rows<D, 256, 256>(dst, ost, S, qrow0, rowc[1], Delta + rbase, tid);
         }
         dst.store(smem + 8 * TB, 1.f, tid);
-        if (dO16) store_tile16(dst, dO16 + base, qrow0, S, tid);
     }
     {
         const int q = qrow0 + tid;
@@ -1366,15 +1316,11 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
 #include "fa2_bwd_dkdv_hs.inc"
 namespace fa2f16b {
 
-// SRC16: Q and dO stream from the 16-bit copies Q16 / dO16 the dQ kernel of the same
-// fa2_backward call wrote (half the bytes per step, no conversion: the staged values are
-// bit for bit the ones the fp32 path converts to)
-template <int D, bool SRC16 = false>
+template <int D>
 __global__ void __launch_bounds__(256, 1)
 fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                        const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-                       float* __restrict__ dK, float* __restrict__ dV, int S, const _Float16* __restrict__ Q16,
-                       const _Float16* __restrict__ dO16) {
+                       float* __restrict__ dK, float* __restrict__ dV, int S) {
     static_assert(D == 64, "hand-scheduled dK/dV: D = 64");
     constexpr int TB = 64 * D, OST = D + 4;
     constexpr int SLOT = FA2_DK_SLOT_D64, RC = FA2_DK_RC_D64, KVB = FA2_DK_KVB_D64;
@@ -1404,23 +1350,13 @@ fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K,
         vst.store(sh + KVB / 2 + 256 * D, 1.f, tid);
     }
     // step 0: Q, dO tiles and the row constants -> slot 0
-    using QStager = typename std::conditional<SRC16, TileStager16<D, 64, 256>, TileStager<D, 64, 256>>::type;
-    QStager qs, ds;
-    if constexpr (SRC16) {
-        qs.init(Q16 + base, S, tid);
-        ds.init(dO16 + base, S, tid);
-        qs.load(0);
-        ds.load(0);
-        qs.store(sh, tid);
-        ds.store(sh + TB, tid);
-    } else {
-        qs.init(Q + base, S, tid);
-        ds.init(dO + base, S, tid);
-        qs.load(0);
-        ds.load(0);
-        qs.store(sh, 1.f, tid);
-        ds.store(sh + TB, 1.f, tid);
-    }
+    TileStager<D, 64, 256> qs, ds;
+    qs.init(Q + base, S, tid);
+    ds.init(dO + base, S, tid);
+    qs.load(0);
+    ds.load(0);
+    qs.store(sh, 1.f, tid);
+    ds.store(sh + TB, 1.f, tid);
     if (tid < 64) {
         float* rc = reinterpret_cast<float*>(lds + RC);
         rc[tid] = tid < S ? -LSE[rbase + tid] * FA2B_LOG2E : 0.f;
@@ -1455,22 +1391,14 @@ fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K,
         float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, wave == 0 ? -FA2B_LOG2E : wave == 1 ? -1.f : 0.f)));
     const int hs_kvb = __builtin_amdgcn_readfirstlane(KVB + wave * 64 * D * 2);
     int hs_cnt = __builtin_amdgcn_readfirstlane(S / 64 - 1);
-    int hs_goff = __builtin_amdgcn_readfirstlane(64 * D * (SRC16 ? 2 : 4));
+    int hs_goff = __builtin_amdgcn_readfirstlane(64 * D * 4);
     int hs_roff = __builtin_amdgcn_readfirstlane(64 * 4);
     (void)SLOT;
-    if constexpr (SRC16) {
 #ifdef FA2_TILE_BF16
-        asm volatile(FA2_DK_ASM_D64_BF16_S16 : FA2_DK_OUTPUTS_D64 : FA2_DK_INPUTS_D64 : FA2_DK_CLOBBERS_D64);
+    asm volatile(FA2_DK_ASM_D64_BF16 : FA2_DK_OUTPUTS_D64 : FA2_DK_INPUTS_D64 : FA2_DK_CLOBBERS_D64);
 #else
-        asm volatile(FA2_DK_ASM_D64_F16_S16 : FA2_DK_OUTPUTS_D64 : FA2_DK_INPUTS_D64 : FA2_DK_CLOBBERS_D64);
+    asm volatile(FA2_DK_ASM_D64_F16 : FA2_DK_OUTPUTS_D64 : FA2_DK_INPUTS_D64 : FA2_DK_CLOBBERS_D64);
 #endif
-    } else {
-#ifdef FA2_TILE_BF16
-        asm volatile(FA2_DK_ASM_D64_BF16 : FA2_DK_OUTPUTS_D64 : FA2_DK_INPUTS_D64 : FA2_DK_CLOBBERS_D64);
-#else
-        asm volatile(FA2_DK_ASM_D64_F16 : FA2_DK_OUTPUTS_D64 : FA2_DK_INPUTS_D64 : FA2_DK_CLOBBERS_D64);
-#endif
-    }
     // dK rows (stage at 0) and dV rows (stage at 256 * OST floats) -> HBM as whole rows
     constexpr int LPR = D / 4, RPI = 64 / LPR;
     const float dscale = 1.f / __builtin_sqrtf((float)D);
@@ -1759,40 +1687,9 @@ hipError_t dkdv_launch(const float* q, const float* k, const float* v, const flo
 // Geometry: 8 waves x 32 keys for D <= 64 (2 waves/SIMD in 256 VGPRs); D = 128 4 x 32
 // (more than 256 registers per lane); fewer waves where the grid would leave CUs idle.
 // Launch-plan overrides (fa2_tune_set, tests and tools only): DKDV_WAVES, DKDV_QS.
-// The hand-scheduled kernels (D = 64): whole 64-row tiles, and a grid of at least one
-// 256-row workgroup per CU (smaller grids keep the wave-split plans).  DQ_HS / DKDV_HS
-// (tests and tools): 1 forces the kernel (an error where it cannot serve), 0 disables it.
-// dK/dV, r06, on 16x16x32 (the r05 32x32x16 form lost inside the step): in one process
-// against the 8-wave kernel, dK/dV -3.1 .. -4.5 % and the fwd + bwd step -1.5 .. -2.1 % at
-// C3, B2_H8_S4096 and B16_H16_S2048, dO = ones and N(0,1) (profiles/r06/dkhs16/).
-template <int D>
-bool dq_hs_plan(long bh, int S) {
-    if constexpr (D != 64) {
-        return false;
-    } else {
-        const int hs = tune_knob("DQ_HS", -1);
-        const bool fits = S % 64 == 0 && S >= 128;
-        return fits && (hs == 1 || (hs < 0 && !tune_knob("DQ_WAVES", 0) && !tune_knob("DQ_KS", 0) &&
-                                    bh * ((S + 255) / 256) >= cu_count()));
-    }
-}
-template <int D>
-bool dkdv_hs_plan(long bh, int S) {
-    if constexpr (D != 64) {
-        return false;
-    } else {
-        const int hs = tune_knob("DKDV_HS", -1);
-        const bool fits = S % 64 == 0 && S >= 128;
-        return fits && (hs == 1 || (hs < 0 && !tune_knob("DKDV_WAVES", 0) && !tune_knob("DKDV_QS", 0) &&
-                                    bh * ((S + 255) / 256) >= cu_count()));
-    }
-}
-// q16 / do16 (the two-kernel plan's hand-off, launch_backward): 16-bit Q and dO copies
-// the dQ kernel wrote, read by the hand-scheduled kernel instead of the fp32 tensors
 template <int D>
 hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
-                         const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream,
-                         const _Float16* q16 = nullptr, const _Float16* do16 = nullptr) {
+                         const float* delta, float* dk, float* dv, int bh, int S, hipStream_t stream) {
     int nw = tune_knob("DKDV_WAVES", 0);  // 0 = auto_waves over the grid of 32-key wave units
     const long units = (long)bh * ((S + 31) / 32);
     // Query groups per workgroup (0 = auto).  Auto, where 8-wave workgroups of one key
@@ -1805,20 +1702,23 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
     // silent launch of another kernel
     if (tune_knob("DKDV_HS", -1) == 1 && (D != 64 || nw || qs)) return hipErrorInvalidValue;
     if constexpr (D == 64) {
-        if (tune_knob("DKDV_HS", -1) == 1 && !(S % 64 == 0 && S >= 128)) return hipErrorInvalidValue;
-        if (dkdv_hs_plan<D>(bh, S)) {
-            const long hgrid = (long)bh * ((S + 255) / 256);
+        // hand-scheduled kernel: whole 64-query steps, and a grid of at least one 256-key
+        // workgroup per CU.  DKDV_HS (tests and tools): 1 forces it (an error where it
+        // cannot serve), 0 disables it.  r06, on 16x16x32 (the r05 32x32x16 form lost inside
+        // the step): in one process against the 8-wave kernel, dK/dV -3.1 .. -4.5 % and the
+        // fwd + bwd step -1.5 .. -2.1 % at C3, B2_H8_S4096 and B16_H16_S2048, dO = ones and
+        // N(0,1) (profiles/r06/dkhs16/)
+        const int hs = tune_knob("DKDV_HS", -1);
+        const bool fits = S % 64 == 0 && S >= 128;
+        if (hs == 1 && !fits) return hipErrorInvalidValue;
+        const long hgrid = (long)bh * ((S + 255) / 256);
+        if (fits && (hs == 1 || (hs < 0 && nw == 0 && qs == 0 && hgrid >= cu_count()))) {
             if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
-            if (q16)
-                hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_hs_kernel<D, true>), dim3((unsigned)hgrid), dim3(256), 0,
-                                   stream, q, k, v, dout, lse, delta, dk, dv, S, q16, do16);
-            else
-                hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_hs_kernel<D, false>), dim3((unsigned)hgrid), dim3(256), 0,
-                                   stream, q, k, v, dout, lse, delta, dk, dv, S, nullptr, nullptr);
+            hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_hs_kernel<D>), dim3((unsigned)hgrid), dim3(256), 0, stream, q, k,
+                               v, dout, lse, delta, dk, dv, S);
             return hipGetLastError();
         }
     }
-    if (q16) return hipErrorInvalidValue;  // the 16-bit copies are read by the hand-scheduled kernel only
     if (qs == 0 && nw == 0 && D <= 64) {
         const int a = auto_waves(units, 8);
         if (a == 4) qs = 2, nw = 8;
@@ -1853,12 +1753,9 @@ hipError_t dq_launch(const float* q, const float* k, const float* v, const float
                            dim3(64 * NW), 0, stream, q, k, v, dout, lse, delta, dq, S, o);
     return hipGetLastError();
 }
-// q16 / do16: the hand-scheduled kernel also writes 16-bit copies of Q and dO there (for
-// the dK/dV kernel of the same launch_backward call)
 template <int D>
 hipError_t dq_dispatch(const float* q, const float* k, const float* v, const float* dout, const float* lse,
-                       float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream,
-                       _Float16* q16 = nullptr, _Float16* do16 = nullptr) {
+                       float* delta, float* dq, int bh, int S, const float* o, hipStream_t stream) {
     // 8 waves (2 per SIMD) for D <= 64; at D = 128 8 waves spill (~120 VGPRs), so 4.
     // Launch-plan overrides (fa2_tune_set, tests and tools only): DQ_WAVES, DQ_KS.
     int nw = tune_knob("DQ_WAVES", 0);  // 0 = auto_waves over the grid of 32-query wave units
@@ -1874,16 +1771,20 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
     int ksp = tune_knob("DQ_KS", 0);
     if (tune_knob("DQ_HS", -1) == 1 && (D != 64 || nw || ksp)) return hipErrorInvalidValue;
     if constexpr (D == 64) {
-        if (tune_knob("DQ_HS", -1) == 1 && !(S % 64 == 0 && S >= 128)) return hipErrorInvalidValue;
-        if (dq_hs_plan<D>(bh, S)) {
-            const long hgrid = (long)bh * ((S + 255) / 256);
+        // hand-scheduled kernel (r05): whole 64-key tiles, and a grid of at least one
+        // 256-row workgroup per CU.  DQ_HS (tests and tools): 1 forces it (an error where it
+        // cannot serve), 0 disables it
+        const int hs = tune_knob("DQ_HS", -1);
+        const bool fits = S % 64 == 0 && S >= 128;
+        if (hs == 1 && !fits) return hipErrorInvalidValue;
+        const long hgrid = (long)bh * ((S + 255) / 256);
+        if (fits && (hs == 1 || (hs < 0 && nw == 0 && ksp == 0 && hgrid >= cu_count()))) {
             if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
             hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D>), dim3((unsigned)hgrid), dim3(256), 0, stream, q, k, v,
-                               dout, lse, delta, dq, S, o, q16, do16);
+                               dout, lse, delta, dq, S, o);
             return hipGetLastError();
         }
     }
-    if (q16) return hipErrorInvalidValue;  // only the hand-scheduled kernel writes the copies
     if (ksp == 0 && nw == 0 && D <= 64) {
         const int a = auto_waves(units, 8);
         if (a == 4) ksp = 2, nw = 8;
@@ -2037,25 +1938,6 @@ hipError_t launch_bwd_fused_delta(int D, const float* q, const float* k, const f
 }
 }  // namespace
 
-namespace {
-// The stream-ordered workspace of launch_backward comes from the device's default memory
-// pool; with the pool's default release threshold (0) its pages would go back to the
-// driver at every synchronisation and be mapped again by the next call.  Keep them.
-void keep_pool_reserved(hipStream_t stream) {
-    static thread_local int done_mask = 0;  // one bit per device seen by this thread
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev >= 31 || (done_mask >> dev & 1)) return;
-    (void)stream;
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t thr = ~0ull;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-    }
-    (void)hipGetLastError();
-    done_mask |= 1 << dev;
-}
-}  // namespace
-
 // Override BWD_FUSED (fa2_tune_set): 1 = Δ kernel, then dK/dV and dQ in one launch (D <= 64);
 // 0 = Δ fused into the dQ kernel's prologue (which stages dO anyway), then dK/dV,
 // which reads it; -1 (default) = 1 on grids of fewer than 8 blocks of 32 rows per
@@ -2068,8 +1950,7 @@ hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* 
     if (fused < 0) fused = bh > 0 && S > 0 && auto_waves((long)bh * ((S + 31) / 32), 8) < 8;
     if (D <= 64 && bh > 0 && S > 0 && fused == 1) {
         // the fused launch has no hand-scheduled roles: forcing one is an error
-        if (tune_knob("DQ_HS", -1) == 1 || tune_knob("DKDV_HS", -1) == 1 || tune_knob("BWD_H16", -1) == 1)
-            return hipErrorInvalidValue;
+        if (tune_knob("DQ_HS", -1) == 1 || tune_knob("DKDV_HS", -1) == 1) return hipErrorInvalidValue;
         // Δ inside the fused launch below 4 blocks of 32 rows per CU (override
         // BWD_FUSED_DELTA; 0 = the separate Δ kernel first).  Measured (B2_H8_D64 fwd +
         // bwd, r02): S = 512 29.9 -> 26.7 us, S = 1024 45.0 -> 40.8; at S = 2048 (4
@@ -2083,36 +1964,6 @@ hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* 
         if (e != hipSuccess) return e;
         e = FA2_TILE_LAUNCH(launch_bwd_fused)(D, q, k, v, dout, lse, delta, dq, dk, dv, bh, S, stream);
         if (e != hipErrorNotSupported) return e;
-    }
-    // Two kernels.  With both hand-scheduled kernels (D = 64, full grids) the dQ kernel,
-    // which stages its Q and dO blocks anyway, also writes them as 16-bit copies into a
-    // stream-ordered workspace (2 * B*H*S*D halves), and the dK/dV kernel streams those:
-    // half its step bytes and no conversion, bit for bit the tiles it would have converted
-    // (override BWD_H16: 1 forces it -- an error where it cannot serve -- 0 disables it;
-    // not while the stream is being captured into a graph)
-    const int h16 = tune_knob("BWD_H16", -1);
-    bool use16 = false;
-    if (D == 64 && h16 != 0 && bh > 0 && S > 0) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        const bool capturing = hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
-        use16 = !capturing && dq_hs_plan<64>(bh, S) && dkdv_hs_plan<64>(bh, S);
-    }
-    if (h16 == 1 && !use16) return hipErrorInvalidValue;
-    if (use16) {
-        const size_t n = (size_t)bh * S * D;
-        _Float16* ws = nullptr;
-        keep_pool_reserved(stream);
-        if (hipMallocAsync(reinterpret_cast<void**>(&ws), 2 * n * sizeof(_Float16), stream) != hipSuccess) {
-            (void)hipGetLastError();
-            if (h16 == 1) return hipErrorOutOfMemory;
-            ws = nullptr;  // the fp32-staging path: the same results
-        }
-        if (ws) {
-            hipError_t e = dq_dispatch<64>(q, k, v, dout, lse, delta, dq, bh, S, o, stream, ws, ws + n);
-            if (e == hipSuccess) e = dkdv_dispatch<64>(q, k, v, dout, lse, delta, dk, dv, bh, S, stream, ws, ws + n);
-            const hipError_t f = hipFreeAsync(ws, stream);
-            return e != hipSuccess ? e : f;
-        }
     }
     hipError_t e = FA2_TILE_LAUNCH(launch_bwd_dq_delta)(D, q, k, v, o, dout, lse, delta, dq, bh, S, stream);
     if (e != hipSuccess) return e;

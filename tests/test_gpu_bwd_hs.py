@@ -55,12 +55,11 @@ def _case(shape, seed=3, gauss=False):
     return (q, k, v, do, eo.astype(np.float32), el.astype(np.float32)), (edq, edk, edv, edl)
 
 
-HS_KNOBS = [{"DQ_HS": 1, "DKDV_HS": 0}, {"DQ_HS": 0, "DKDV_HS": 1}, {"DQ_HS": 1, "DKDV_HS": 1, "BWD_H16": 0},
-            {"DQ_HS": 1, "DKDV_HS": 1, "BWD_H16": 1}]
+HS_KNOBS = [{"DQ_HS": 1, "DKDV_HS": 0}, {"DQ_HS": 0, "DKDV_HS": 1}, {"DQ_HS": 1, "DKDV_HS": 1}]
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-@pytest.mark.parametrize("knobs", HS_KNOBS, ids=["dq_hs", "dkdv_hs", "both_hs", "both_hs_h16"])
+@pytest.mark.parametrize("knobs", HS_KNOBS, ids=["dq_hs", "dkdv_hs", "both_hs"])
 @pytest.mark.parametrize("shape", DQ_SHAPES + [(1, 1, 384, 64), (1, 1, 448, 64)], ids=lambda s: "B%d_H%d_S%d_D%d" % s)
 def test_hs_full_backward(shape, knobs, precision):
     """fa2_backward's two-kernel plan with the hand-scheduled dQ (Δ fused, written out for
@@ -190,43 +189,6 @@ def test_hs_bwd_forced_at_other_head_dims_is_an_error(knob):
     fa2amd.tune_set(knob, 1)
     fa2amd.tune_set("BWD_FUSED", 0)
     (q, k, v, do, o, lse), _ = _case((1, 2, 256, 32))
-    tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
-    with pytest.raises(fa2amd.FA2Error):
-        fa2amd.backward(tq, tk, tv, to, tdo, tl, "fp16")
-
-
-@pytest.mark.parametrize("precision", ["fp16", "bf16"])
-def test_h16_handoff_is_bitwise_the_fp32_staging(precision):
-    """fa2_backward's two-kernel plan hands the dK/dV kernel 16-bit copies of Q and dO that
-    the dQ kernel wrote (BWD_H16, the default on full grids): the staged tiles are the same
-    bits the dK/dV kernel converts from fp32 itself, so dQ, dK and dV are bitwise equal with
-    and without the hand-off (C3 shape, dO ~ N(0,1)); and the default is the hand-off."""
-    B, H, S, D = 4, 16, 2048, 64
-    q, k, v = fo.harness_inputs(B, H, S, D, seed=6)
-    do = np.random.RandomState(12).randn(B, H, S, D).astype(np.float32)
-    tq, tk, tv, tdo = cuda(q, k, v, do)
-    o, lse = fa2amd.forward(tq, tk, tv, precision)
-    res = []
-    for h16 in (1, 0, -1):
-        fa2amd.tune_set("BWD_H16", h16)
-        g = fa2amd.backward(tq, tk, tv, o, tdo, lse, precision)
-        torch.cuda.synchronize()
-        res.append([x.cpu().numpy() for x in g])
-    for a, b, c in zip(*res):
-        assert np.array_equal(a, b) and np.array_equal(a, c)
-    edq, edk, edv, _ = fo.attention_backward(q[:1, :1], k[:1, :1], v[:1, :1], do[:1, :1])
-    for got, exp in zip(res[0], (edq, edk, edv)):
-        assert maxerr(got[:1, :1], exp) < TOL[precision] * max(1.0, float(np.abs(exp).max()))
-
-
-@pytest.mark.parametrize("knobs", [{"DKDV_HS": 0, "BWD_FUSED": 0}, {"DQ_HS": 0, "BWD_FUSED": 0}, {"BWD_FUSED": 1}, {}],
-                         ids=["dkdv_8wave", "dq_8wave", "fused", "small_grid_auto"])
-def test_h16_forced_where_it_cannot_serve_is_an_error(knobs):
-    """BWD_H16 = 1 needs both hand-scheduled kernels in the two-kernel plan"""
-    fa2amd.tune_set("BWD_H16", 1)
-    for key, val in knobs.items():
-        fa2amd.tune_set(key, val)
-    (q, k, v, do, o, lse), _ = _case((1, 2, 256, 64))
     tq, tk, tv, tdo, to, tl = cuda(q, k, v, do, o, lse)
     with pytest.raises(fa2amd.FA2Error):
         fa2amd.backward(tq, tk, tv, to, tdo, tl, "fp16")
