@@ -252,7 +252,7 @@ def fix_hazards(block, preds):
 
 
 ABL = set()  # timing-only ablations (--abl a,b --out file): results are invalid, never the product .inc
-EXACT_ABL = {"addrr", "nospread", "vsum", "pkmul32"}  # variants that keep the product's results (and its flag)
+EXACT_ABL = {"addrr", "nospread", "vsum", "pkmul32", "convp1"}  # variants that keep the product's results (and its flag)
 
 
 def ablate(seq):

@@ -286,7 +286,12 @@ def body(cfg, j3, log):
     conv = staging_convert(cfg, n)
     for i in conv:
         i.earliest = 2
-    seq += schedule_phase(cfg, sdp_mfmas(cfg, 0), [pds_part(cfg, 1, 1), conv, pre], f"P1.{j3}", log)
+    # the staging convert in P2 (the lightest phase: 47 fillers against P1's 78) and the next
+    # step's loads over P3, P4: step -0.6 .. +0.1 % (5 of 6 cases <= 0), kernel -0.2 .. -1.8 %
+    # in one process (profiles/r06/convp2/); 'convp1' keeps the old placement
+    convp2 = "convp1" not in asmgen.ABL
+    seq += schedule_phase(cfg, sdp_mfmas(cfg, 0), [pds_part(cfg, 1, 1)] + ([] if convp2 else [conv]) + [pre],
+                          f"P1.{j3}", log)
     # P2: dV, dK of B (j-1) | P, dS of A key blocks 0, 1; B's seeds for P3; loads of step j+2
     #     (staging registers free since P1's convert) spread over P2, P3, P4, the offset adds
     #     after the last of them
@@ -294,10 +299,16 @@ def body(cfg, j3, log):
     stl = staging_loads(cfg)
     if "nospread" in asmgen.ABL:
         ld = (stl, [], [])
+    elif convp2:
+        h = (len(stl) - 2 + 1) // 2
+        ld = ([], stl[:h], stl[h:])
+        for i in conv:
+            i.earliest = 0
     else:
         ld = thirds(stl[:-2])
         ld = (ld[0], ld[1], ld[2] + stl[-2:])
-    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 1), [pds_part(cfg, 0, 0), sd, list(ld[0])], f"P2.{j3}", log)
+    seq += schedule_phase(cfg, dkdv_mfmas(cfg, 1), [pds_part(cfg, 0, 0), sd] + ([conv] if convp2 else []) + [list(ld[0])],
+                          f"P2.{j3}", log)
     # P3: S, dP of B | P, dS of A key blocks 2, 3; A's trop frags for P4 (the ring is free
     #     after P2)
     pre = []
