@@ -37,8 +37,8 @@ Register map (per wave, D = head dim, NB = D/32, NTQ = D/16, CPT = D/32):
         Vf[i]        a[32NB+8NTQ + 4i]        Vᵀ fragments of one tile (A operand of PV)
   VGPR  S[c][kb]     v[32c + 16kb]            Sᵀ accumulators; exps and packed P in place
         NM[c]        v[64 + 16c]              -m splat: the C operand of each QKᵀ chain
-        Kf ring      v[96 + 4r], r < 8        K fragments (A operand of QKᵀ)
-        staging      v[128 ...]               fp32 K then V rows of the next tile
+        Kf ring      v[96 + 4r], r < ring     K fragments (A operand of QKᵀ); 8 slots, 12 at D = 128
+        staging      v[96 + 4 ring ...]       fp32 K then V rows of the next tile
         misc         m, l, tile partial sums, temporaries
 
 Usage: python3 gen_fwd_hs.py [--check]   (--check: verify the .inc is up to date)
@@ -65,12 +65,18 @@ class Cfg:
         self.NB, self.NTQ, self.CPT = D // 32, D // 16, D // 32
         self.NF = 4 * self.NB  # V fragments per tile
         self.NKF = 2 * self.NTQ  # K fragments per tile
-        self.ring = 8  # K fragment ring slots
+        # K fragment ring slots.  D = 128 (16 fragments per tile): 12 slots, so chain B's QKᵀ
+        # re-reads only the 4 fragments chain A's overflow reads overwrote (20 b128 fragment
+        # reads per tile instead of 32); the 'ring8' build keeps the r05 ring of 8
+        self.ring = 12 if D == 128 and "ring8" not in asmgen.ABL else 8
         self.keep_k = self.NKF <= self.ring  # D = 64: all K fragments stay for both QKᵀ
+        # overflow fragments per tile; 'big ring' order when they fit half a key block
+        self.ovf = self.NKF - self.ring
+        self.bigring = not self.keep_k and self.ovf <= self.NTQ // 2
         self.QB = 32 * self.NB
         self.VB = self.QB + 8 * self.NTQ
         self.nagpr = self.VB + 4 * self.NF
-        self.STG = 128
+        self.STG = 96 + 4 * self.ring
         self.MB = self.STG + 16 * self.CPT
         self.nvgpr = self.MB + 16
         self.SV = self.nvgpr  # 'stamps' timing builds: the stamp register (and one more)
@@ -182,15 +188,36 @@ def vfrag_reads(cfg, i, slot, earliest=0):
     ])
 
 
-def qk_mfmas(cfg, c, kreg):
-    """Sᵀ[c] = K Qᵀ[c] - m[c]: kb-major chains (kb = 0 finishes first)"""
-    out = []
-    for kb in range(2):
-        for t in range(cfg.NTQ):
-            f = kb * cfg.NTQ + t
-            cc = ("v", cfg.NM(c)) if t == 0 else ("v", cfg.S(c, kb))
-            out.append(mfma(cfg, ("v", cfg.S(c, kb)), ("v", kreg(f)), ("a", cfg.Q(c, t)), cc))
+def qk_mfmas(cfg, c, kreg, order=None):
+    """Sᵀ[c] = K Qᵀ[c] - m[c]: kb-major chains (kb = 0 finishes first), or the (kb, t)
+    `order` given; the first MFMA of each kb takes the -m splat as its C operand"""
+    order = order or [(kb, t) for kb in range(2) for t in range(cfg.NTQ)]
+    out, seeded = [], set()
+    for kb, t in order:
+        f = kb * cfg.NTQ + t
+        cc = ("v", cfg.S(c, kb)) if kb in seeded else ("v", cfg.NM(c))
+        seeded.add(kb)
+        out.append(mfma(cfg, ("v", cfg.S(c, kb)), ("v", kreg(f)), ("a", cfg.Q(c, t)), cc))
     return out
+
+
+def bigring_b(cfg):
+    """chain B's QKᵀ order and fragment registers with the big ring (ovf = x overflow
+    fragments): chain A's P1 put fragments ring.. into slots 0..x-1, so B runs kb 0 from
+    t = x, then kb 1's fragments still in their slots, then kb 0's first x fragments
+    re-read into the slots of kb 0's first x (free after B's first x MFMAs), then the
+    overflow fragments; kb 0 still finishes 4 MFMAs before the phase ends"""
+    x, NTQ = cfg.ovf, cfg.NTQ
+    order = [(0, t) for t in range(x, NTQ)] + [(1, t) for t in range(NTQ - x)] + \
+            [(0, t) for t in range(x)] + [(1, t) for t in range(NTQ - x, NTQ)]
+
+    def kreg(f):
+        if f < x:
+            return cfg.Kr(x + f)
+        return cfg.Kr(f - cfg.ring) if f >= cfg.ring else cfg.Kr(f)
+    # re-read i: into slot x + i after B's MFMA i used it, before B's MFMA 2(NTQ - x) + i
+    windows = [(i, i + 1, 2 * (NTQ - x) + i - 3) for i in range(x)]
+    return order, kreg, windows
 
 
 def qk_mfmas_zero(cfg, c, kreg):
@@ -339,17 +366,24 @@ def body(cfg, p, log):
     seq += schedule_phase(cfg, qk_mfmas(cfg, 0, ring), [softmax_part(cfg, 1, 1, True), kreads, conv], f"P1.{p}", log)
     seq += stamp(cfg.SV)
     # P2: PV of chain B (tile j-1) | softmax A (j) first half, V(j+1) staged, K(j+2) loads,
-    #     K re-read 0..7 (D=128), first V(j) fragments into freed Vf slots
+    #     K re-read 0..7 (D = 128, ring of 8), first V(j) fragments into freed Vf slots
     nsplit = cfg.NF // 4 if cfg.D > 64 else 0
     vre = []
     for i in range(nsplit):
         vre += vfrag_reads(cfg, i, p, earliest=i + 2)
-    rer = [] if cfg.keep_k else [kfrag_read(cfg, f, p, cfg.Kr(f)) for f in range(cfg.ring)]
+    rer = [] if cfg.keep_k or cfg.bigring else [kfrag_read(cfg, f, p, cfg.Kr(f)) for f in range(cfg.ring)]
     seq += schedule_phase(cfg, pv_mfmas(cfg, 1), [softmax_part(cfg, 0, 0, False), staging_convert(cfg, 1, q),
                                                   ld[0], rer, vre], f"P2.{p}", log)
-    # P3: QKᵀ of chain B (tile j) | softmax A (j) second half, K fragments 8.. (D=128), rest of V(j)
+    # P3: QKᵀ of chain B (tile j) | softmax A (j) second half, K re-reads (D = 128), rest of V(j)
     kreads = []
-    if not cfg.keep_k:
+    order_b, kreg_b = None, ring
+    if cfg.bigring:
+        order_b, kreg_b, windows = bigring_b(cfg)
+        for f, lo, hi in windows:
+            ins = kfrag_read(cfg, f, p, kreg_b(f))
+            ins.earliest, ins.deadline = lo, hi
+            kreads.append(ins)
+    elif not cfg.keep_k:
         for f in range(cfg.ring, NKF):
             r = f - cfg.ring
             ins = kfrag_read(cfg, f, p, cfg.Kr(r))
@@ -359,8 +393,8 @@ def body(cfg, p, log):
     for i in range(nsplit, cfg.NF):
         vre += vfrag_reads(cfg, i, p)
     seq += stamp(cfg.SV)
-    seq += schedule_phase(cfg, qk_mfmas(cfg, 1, ring), [softmax_part(cfg, 0, 1, True), kreads, vre, list(ld[1])],
-                          f"P3.{p}", log)
+    seq += schedule_phase(cfg, qk_mfmas(cfg, 1, kreg_b, order_b), [softmax_part(cfg, 0, 1, True), kreads, vre,
+                                                                   list(ld[1])], f"P3.{p}", log)
     seq.append(Ins("s_waitcnt lgkmcnt(0)", "wait"))
     seq += stamp(cfg.SV)
     seq.append(Ins("s_barrier", "bar"))
