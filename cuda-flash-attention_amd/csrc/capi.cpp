@@ -66,7 +66,8 @@ std::atomic<int> g_tune_n{0};
 // so a misspelt knob cannot silently leave an A/B on the default plan)
 const char* const kKnobs[] = {"FWD_HS",   "FWD_WAVES", "FWD_KS",          "FWD_NKB", "DKDV_WAVES", "DKDV_QS",
                               "DKDV_HS",  "DQ_WAVES",  "DQ_KS",           "DQ_HS",   "BWD_FUSED",  "BWD_FUSED_DELTA",
-                              "BWD_FQS",  "BWD_FKS",   "BWD_FNW",         "HOST_SHARDS_ON_DEVICE0",    "HOST_CHUNKS"};
+                              "BWD_FQS",  "BWD_FKS",   "BWD_FNW",         "HOST_SHARDS_ON_DEVICE0",    "HOST_CHUNKS",
+                              "FWD_SPLIT"};
 bool known_knob(const char* k) {
     for (const char* n : kKnobs)
         if (!strcmp(n, k)) return true;
@@ -97,6 +98,67 @@ int cu_count() {
     return ncu;
 }
 
+// per-(device, stream) scratch of the split plans (f-attn2.cuh: stream_scratch)
+struct StreamScratch {
+    int device;
+    hipStream_t stream;
+    void* p;
+    size_t bytes;
+};
+std::mutex g_scr_mu;
+std::vector<StreamScratch> g_scr;    // eager calls' blocks, one per (device, stream)
+std::vector<StreamScratch> g_scr_g;  // blocks handed to graph captures (owned by the graphs)
+
+void* stream_scratch(hipStream_t stream, size_t bytes) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lock(g_scr_mu);
+    if (cs != hipStreamCaptureStatusNone) {
+        // a capture cannot allocate: it takes the stream's block from an earlier eager call
+        // (the usual warm-up before a capture), which then belongs to the graph -- later eager
+        // calls get a block of their own, so a replay and eager work never share one
+        for (size_t i = 0; i < g_scr.size(); ++i)
+            if (g_scr[i].device == dev && g_scr[i].stream == stream && g_scr[i].bytes >= bytes) {
+                g_scr_g.push_back(g_scr[i]);
+                g_scr.erase(g_scr.begin() + (long)i);
+                return g_scr_g.back().p;
+            }
+        return nullptr;
+    }
+    for (auto& e : g_scr) {
+        if (e.device != dev || e.stream != stream) continue;
+        if (e.bytes >= bytes) return e.p;
+        // grow: the stream's earlier launches may still read the old block
+        if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+        (void)hipFree(e.p);
+        e.p = nullptr;
+        e.bytes = 0;
+        if (hipMalloc(&e.p, bytes) != hipSuccess) return e.p = nullptr;
+        e.bytes = bytes;
+        return e.p;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    g_scr.push_back({dev, stream, p, bytes});
+    return p;
+}
+
+void stream_scratch_release() {
+    int dev0 = 0;
+    const bool have = hipGetDevice(&dev0) == hipSuccess;
+    std::lock_guard<std::mutex> lock(g_scr_mu);
+    for (auto* v : {&g_scr, &g_scr_g}) {
+        for (auto& e : *v) {
+            (void)hipSetDevice(e.device);
+            (void)hipFree(e.p);
+        }
+        v->clear();
+    }
+    if (have) (void)hipSetDevice(dev0);
+}
+
 int auto_waves(long blocks32, int maxnw, int minnw) {
     const int ncu = cu_count();
     for (int nw = maxnw; nw > minnw; nw /= 2)
@@ -107,7 +169,7 @@ int auto_waves(long blocks32, int maxnw, int minnw) {
 
 extern "C" {
 
-int fa2_version(void) { return 2 * 10000 + 0 * 100 + 0; }  // 2.0: fa2_backward_ws removed
+int fa2_version(void) { return 2 * 10000 + 1 * 100 + 0; }  // 2.1: split forward, per-stream scratch
 
 #ifndef FA2_BUILD_ID
 #define FA2_BUILD_ID "unknown"
@@ -520,6 +582,7 @@ int fa2_host_release(void) {
         }
     }
     if (have) (void)hipSetDevice(dev0);
+    fa2::stream_scratch_release();
     return FA2_OK;
 }
 

@@ -137,4 +137,12 @@ int auto_waves(long blocks32, int maxnw, int minnw = 2);
 // Compute units of the current device (cached per device).
 int cu_count();
 
+// Device scratch of the split launch plans: one grow-only buffer per (device, stream),
+// kept between calls (fa2_host_release frees it).  While `stream` is being captured into
+// a graph (a capture must not allocate) the stream's block from an earlier eager call
+// moves to the graph, or nullptr when there is none big enough; nullptr too when the
+// allocation fails.  The auto plans then fall back to their unsplit form.
+void* stream_scratch(hipStream_t stream, size_t bytes);
+void stream_scratch_release();
+
 }  // namespace fa2

@@ -806,10 +806,31 @@ fa2_fwd_f16_kernel(const float* __restrict__ Q, const float* __restrict__ K, con
 #include "fa2_fwd_hs.inc"
 namespace fa2f16 {
 
+// Split partials (KSPLIT = P > 1 key chunks of L = S / P keys per head): chunk c of head
+// bh leaves, per query row, its unnormalised O row at part + ((c*BH + bh)*S + row)*D and
+// (m, l) -- the chunk's row reference (log2 units) and row sum -- at
+// part + P*BH*S*D + ((c*BH + bh)*S + row)*2; fa2_fwd_merge_kernel combines them.
+template <int D>
+__device__ __forceinline__ void fwd_store_part(const FwdState<D>& st, float* part_o, float* part_ml, int q, int S,
+                                               int h) {
+    const float lt = xor32_sum((st.l[0] + st.l[1]) + (st.l[2] + st.l[3]));
+    if (q < S) {
+        float* orow = part_o + (long)q * D;
+#pragma unroll
+        for (int b = 0; b < D / 32; ++b)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 v = {st.oacc[b][4 * g], st.oacc[b][4 * g + 1], st.oacc[b][4 * g + 2], st.oacc[b][4 * g + 3]};
+                *reinterpret_cast<f32x4*>(orow + 32 * b + 8 * g + 4 * h) = v;
+            }
+        if (h == 0) *reinterpret_cast<float2*>(part_ml + 2L * q) = make_float2(st.m, lt);
+    }
+}
+
 template <int D>
 __global__ void __launch_bounds__(256, 1)
 fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
-                  float* __restrict__ O, float* __restrict__ LSE, int S) {
+                  float* __restrict__ O, float* __restrict__ LSE, int S, int P, float* __restrict__ part) {
     static_assert(D == 64 || D == 128, "hand-scheduled forward: D = 64 or 128");
     constexpr int KT = 64, TB = KT * D;  // halves per tile image
     constexpr int OST = D + 4;           // O stage row stride (floats), as in the generator
@@ -820,16 +841,25 @@ fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, cons
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nqb = (S + 255) / 256;
+    // workgroup -> (head, key chunk, query block): the query blocks of one chunk are
+    // consecutive, so after the XCD remap they share one L2's copy of the chunk's K/V
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = bid / nqb, qb = bid - bh * nqb;
+    const int qb = bid % nqb, bc = bid / nqb;
+    const int bh = bc / P, kc = bc - bh * P;
     const long base = (long)bh * S * D;
     const int qrow0 = qb * 256;
+    const int L = S / P;            // keys of this workgroup's chunk (S itself when P = 1)
+    const long kbase = base + (long)kc * L * D;
+    // P > 1: this chunk's partial rows (see fwd_store_part)
+    const long prow = ((long)kc * (gridDim.x / (P * nqb)) + bh) * S;
+    float* part_o = P > 1 ? part + prow * D : nullptr;
+    float* part_ml = P > 1 ? part + (long)gridDim.x / nqb * S * D + prow * 2 : nullptr;
 
     // Q block (256 rows, scaled by log2(e)/sqrt(D)) -> LDS [4TB, 8TB) halves; K(0), V(0)
     // -> slot 0 of the K and V rings ([0, TB) and [2TB, 3TB))
     TileStager<D, KT, 256> ks, vs;
-    ks.init(K + base, S, tid);
-    vs.init(V + base, S, tid);
+    ks.init(K + kbase, L, tid);
+    vs.init(V + kbase, L, tid);
     {
         TileStager<D, 256, 256> qst;
         qst.init(Q + base, S, tid);
@@ -858,7 +888,7 @@ fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, cons
     const int hs_oa = ((wave * 64 + r) * OST + 4 * h) * 4;
     const __amdgpu_buffer_rsrc_t hs_rsk = ks.rs, hs_rsv = vs.rs;
     const int hs_qb = __builtin_amdgcn_readfirstlane(4 * TB * 2 + wave * 64 * D * 2);
-    int hs_cnt = __builtin_amdgcn_readfirstlane(S / KT - 1);
+    int hs_cnt = __builtin_amdgcn_readfirstlane(L / KT - 1);
     int hs_goff = __builtin_amdgcn_readfirstlane(KT * D * 4);
     float hs_m0, hs_m1, hs_l0, hs_l1;
     unsigned long long hs_flag;
@@ -879,7 +909,23 @@ fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, cons
     // hs_flag is a scalar (wave-uniform): this wave saw a half-row sum out of range
     const bool wave_bad = hs_flag != 0;
     const bool any_bad = __syncthreads_or(wave_bad);
-    if (!wave_bad) {
+    if (!wave_bad && P > 1) {
+        // a key chunk's partial: the unnormalised O rows from the stage, (m, l) per row
+        const float lt0 = xor32_sum(hs_l0), lt1 = xor32_sum(hs_l1);
+        const int q0 = qrow0 + wave * 64 + r;
+        if (h == 0) {
+            if (q0 < S) *reinterpret_cast<float2*>(part_ml + 2L * q0) = make_float2(hs_m0, lt0);
+            if (q0 + 32 < S) *reinterpret_cast<float2*>(part_ml + 2L * (q0 + 32)) = make_float2(hs_m1, lt1);
+        }
+        constexpr int LPR = D / 4, RPI = 64 / LPR;
+        const float* os = reinterpret_cast<const float*>(smem);
+#pragma unroll 4
+        for (int rr = 0; rr < 64; rr += RPI) {
+            const int row = wave * 64 + rr + lane / LPR, c4 = (lane % LPR) * 4;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(os + row * OST + c4);
+            if (qrow0 + row < S) *reinterpret_cast<f32x4*>(part_o + (long)(qrow0 + row) * D + c4) = v;
+        }
+    } else if (!wave_bad) {
         // O rows [wave*64 + c*32 + q][OST] (unnormalised) are in the stage; l is per lane
         // half: the xor-32 sum is the row's total
         const float lt0 = xor32_sum(hs_l0), lt1 = xor32_sum(hs_l1);
@@ -914,7 +960,7 @@ fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, cons
         fwd_init<D>(st[0], Q, base, q, S, h);
         fwd_init<D>(st[1], Q, base, q + 32, S, h);
     }
-    const int ntiles = (S + KT - 1) / KT;
+    const int ntiles = L / KT;
 #pragma unroll 1
     for (int j = 0; j < ntiles; ++j) {
         ks.load(j * KT);
@@ -926,13 +972,43 @@ fa2_fwd_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, cons
         if (wave_bad) {
             f32x16 sacc[2][2];
             fwd_qk<D, 2, 2, true>(sacc, st, smem, fo);
-            fwd_softmax_pv<D, 2, false, 2, true>(st, sacc, smem + TB, fo, j * KT, S, h, j == 0);
+            fwd_softmax_pv<D, 2, false, 2, true>(st, sacc, smem + TB, fo, j * KT, L, h, j == 0);
         }
     }
-    if (wave_bad) {
+    if (wave_bad && P > 1) {
+        fwd_store_part<D>(st[0], part_o, part_ml, q, S, h);
+        fwd_store_part<D>(st[1], part_o, part_ml, q + 32, S, h);
+    } else if (wave_bad) {
         fwd_store<D>(st[0], O, LSE, base, (long)bh * S, q, S, h);
         fwd_store<D>(st[1], O, LSE, base, (long)bh * S, q + 32, S, h);
     }
+}
+
+// Merge of the P key-chunk partials of fa2_fwd_hs_kernel (layout at fwd_store_part), in
+// chunk order (deterministic): M = max m_c, w_c = 2^(m_c - M), O = sum w_c O_c / sum w_c l_c,
+// LSE = M ln 2 + ln(sum w_c l_c).  One thread per 4 columns of a row.
+template <int D>
+__global__ void __launch_bounds__(256)
+fa2_fwd_merge_kernel(const float* __restrict__ part, int P, long rows, float* __restrict__ O,
+                     float* __restrict__ LSE) {
+    constexpr int C4 = D / 4;
+    const long x = (long)blockIdx.x * 256 + threadIdx.x;
+    if (x >= rows * C4) return;
+    const long row = x / C4;
+    const int c4 = (int)(x - row * C4) * 4;
+    const float2* ml = reinterpret_cast<const float2*>(part + (long)P * rows * D);
+    float M = -__builtin_inff();
+    for (int c = 0; c < P; ++c) M = fmaxf(M, ml[c * rows + row].x);
+    float l = 0.f;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < P; ++c) {
+        const float2 e = ml[c * rows + row];
+        const float w = exp2f(e.x - M);
+        l += w * e.y;
+        o += w * *reinterpret_cast<const f32x4*>(part + (c * rows + row) * D + c4);
+    }
+    *reinterpret_cast<f32x4*>(O + row * D + c4) = o * (1.f / l);
+    if (c4 == 0) LSE[row] = M * FA2_LN2 + __logf(l);
 }
 #endif  // CUPY_INLINE_COMPILE
 
@@ -1026,13 +1102,43 @@ static hipError_t fwd_f16_launch(const float* q, const float* k, const float* v,
     return hipGetLastError();
 }
 
+// P > 1: each head's keys in P chunks of S / P (a multiple of 64, >= 128) on their own
+// workgroups, partials in `part` (P * bh * S * (D + 2) floats), then the merge pass
 template <int D>
 static hipError_t fwd_hs_launch(const float* q, const float* k, const float* v, float* o, float* lse, int bh, int S,
-                                hipStream_t stream) {
-    const long grid = (long)bh * ((S + 255) / 256);
+                                hipStream_t stream, int P = 1, float* part = nullptr) {
+    if (P < 1 || S % (64 * P) || S / P < 128 || (P > 1 && !part)) return hipErrorInvalidValue;
+    const long grid = (long)bh * ((S + 255) / 256) * P;
     if (grid <= 0 || grid > 0x7fffffffL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((fa2f16::fa2_fwd_hs_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, o, lse, S);
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_hs_kernel<D>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, o, lse, S,
+                       P, part);
+    if (P == 1) return hipGetLastError();
+    const long rows = (long)bh * S, threads = rows * (D / 4);
+    hipLaunchKernelGGL((fa2f16::fa2_fwd_merge_kernel<D>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       stream, part, P, rows, o, lse);
     return hipGetLastError();
+}
+
+// Key chunks per head for a grid of `g` 256-row workgroups that leaves CUs idle: the
+// most chunks (a power of two, at most 4) that keep the grid within one workgroup per
+// CU and chunks of at least 1024 keys (D = 64) / 256 keys (D = 128), for heads of at
+// least 4096 / 1024 keys; 1 where no split applies.  r06 in-process A/B of the forward
+// (profiles/r06/split/), unsplit small-grid plan -> split:
+//   D = 64:  B1_H2_S4096 38.2 -> 26.9 us (P = 4), B1_H4_S4096 39.7 -> 34.2 (4),
+//            B1_H2_S8192 74.3 -> 46.0 (4); P = 2 (B1_H8_S4096) and S = 2048 at 4-16 heads
+//            tie or lose 3-20 % (the merge pass and the partial rows' traffic grow with
+//            the workgroups while the unsplit workgroups stream only 2048 keys);
+//   D = 128: the small-grid plans are weaker (4 / 8 waves of ~400 VGPRs): B1_H2_S1024
+//            31.8 -> 20.0 (4), B1_H2_S2048 57.6 -> 27.5 (4), B1_H8_S2048 59.8 -> 37.2 (4),
+//            B2_H8_S2048 66.9 -> 51.1 (2), B1_H8_S4096 124.7 -> 78.2 (2), B2_H8_S1024
+//            33.8 -> 30.8 (4); S = 512 loses (19.0 -> 20.9).
+static int fwd_split_auto(int D, long g, int S) {
+    const int min_s = D == 128 ? 1024 : 4096, min_chunk = D == 128 ? 256 : 1024;
+    if (S < min_s) return 1;
+    const long ncu = cu_count();
+    int P = 1;
+    while (P < 4 && g * (2 * P) <= ncu && S % (64 * 2 * P) == 0 && S / (2 * P) >= min_chunk) P *= 2;
+    return D == 64 && P < 4 ? 1 : P;
 }
 
 template <int D>
@@ -1050,10 +1156,27 @@ static hipError_t fwd_f16_dispatch(const float* q, const float* k, const float* 
         const bool forced_other = tune_knob("FWD_WAVES", 0) || tune_knob("FWD_KS", 0) || tune_knob("FWD_NKB", 0);
         // a forced FWD_HS the plan cannot take (shape, or other plan knobs) is an error
         if (hs == 1 && (!fits || forced_other)) return hipErrorInvalidValue;
-        if (fits && (hs == 1 || (hs < 0 && !forced_other && (long)bh * ((S + 255) / 256) >= cu_count())))
+        const long g = (long)bh * ((S + 255) / 256);
+        // FWD_SPLIT (tests and tools): P >= 2 forces P key chunks per head on the
+        // hand-scheduled kernel (an error where it cannot serve: shape, other plan knobs,
+        // FWD_HS = 0, or no scratch -- a stream being captured), 1 disables the split,
+        // 0 = auto (grids below one workgroup per CU, fwd_split_auto)
+        const int split = tune_knob("FWD_SPLIT", 0);
+        if (split < 0) return hipErrorInvalidValue;
+        if (split >= 2 && (!fits || forced_other || hs == 0 || S % (64 * split) || S / split < 128))
+            return hipErrorInvalidValue;
+        int P = split >= 2 ? split : 1;
+        if (split == 0 && fits && hs < 0 && !forced_other && g < cu_count()) P = fwd_split_auto(D, g, S);
+        if (P > 1) {
+            float* part = static_cast<float*>(stream_scratch(stream, sizeof(float) * P * (size_t)bh * S * (D + 2)));
+            if (part) return fwd_hs_launch<D>(q, k, v, o, lse, bh, S, stream, P, part);
+            if (split >= 2) return hipErrorInvalidValue;
+        }
+        if (fits && (hs == 1 || (hs < 0 && !forced_other && g >= cu_count())))
             return fwd_hs_launch<D>(q, k, v, o, lse, bh, S, stream);
     } else {
-        if (tune_knob("FWD_HS", -1) == 1) return hipErrorInvalidValue;  // no hand-scheduled kernel at this D
+        // no hand-scheduled kernel at this D
+        if (tune_knob("FWD_HS", -1) == 1 || tune_knob("FWD_SPLIT", 0) >= 2) return hipErrorInvalidValue;
     }
     // 8 waves (2 per SIMD) where the registers allow it; D = 128 runs 4 waves of
     // ~400 VGPRs (8 would spill and exceed the LDS budget with the Q stages)

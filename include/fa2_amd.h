@@ -109,7 +109,10 @@ int fa2_fa1_forward(const float* q, const float* k, const float* v, float* o, fl
  * scratch is kept between calls (one grow-only block per device); each shard runs
  * as a pipeline over head chunks, the H2D of the next chunk and the D2H of the
  * previous one overlapping the current chunk's kernels.  fa2_host_release frees
- * the scratch (the next call allocates it again).
+ * the scratch (the next call allocates it again), and also the per-stream scratch
+ * the device-pointer calls keep for their split launch plans (small grids), including
+ * the blocks graphs captured from those calls hold; call it with no work of this library
+ * in flight and no such graph left to replay.
  * ------------------------------------------------------------------------- */
 int fa2_forward_host(const float* q, const float* k, const float* v, float* o, float* lse, int batch, int heads,
                      int seq, int head_dim, int precision, int num_devices, float* kernel_ms);
@@ -126,7 +129,7 @@ int fa2_shard_range(int total_heads, int shards, int index, int* first, int* cou
 /* Launch-plan override (tests and tuning tools only; nothing is read from the
  * environment).  fa2_tune_set("DKDV_QS", 2) makes the next launches use that plan
  * where the shape allows it; fa2_tune_set(NULL, 0) clears every override.  Knobs:
- * FWD_HS, FWD_WAVES, FWD_KS, FWD_NKB, DKDV_HS, DKDV_WAVES, DKDV_QS, DQ_HS, DQ_WAVES,
+ * FWD_HS, FWD_SPLIT, FWD_WAVES, FWD_KS, FWD_NKB, DKDV_HS, DKDV_WAVES, DKDV_QS, DQ_HS, DQ_WAVES,
  * DQ_KS, BWD_FUSED, BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW (see the launchers in
  * kernels/; a value that forces a plan the shape cannot take is FA2_E_INVALID at the
  * launch, never a silent fallback), and

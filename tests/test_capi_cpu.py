@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version():
-    assert fa2amd.version() == 20000
+    assert fa2amd.version() == 20100
 
 
 def test_tune_overrides_validated_and_restored():
