@@ -67,7 +67,7 @@ std::atomic<int> g_tune_n{0};
 const char* const kKnobs[] = {"FWD_HS",   "FWD_WAVES", "FWD_KS",          "FWD_NKB", "DKDV_WAVES", "DKDV_QS",
                               "DKDV_HS",  "DQ_WAVES",  "DQ_KS",           "DQ_HS",   "BWD_FUSED",  "BWD_FUSED_DELTA",
                               "BWD_FQS",  "BWD_FKS",   "BWD_FNW",         "HOST_SHARDS_ON_DEVICE0",    "HOST_CHUNKS",
-                              "FWD_SPLIT"};
+                              "FWD_SPLIT", "BWD_SPLIT"};
 bool known_knob(const char* k) {
     for (const char* n : kKnobs)
         if (!strcmp(n, k)) return true;
@@ -104,6 +104,7 @@ struct StreamScratch {
     hipStream_t stream;
     void* p;
     size_t bytes;
+    unsigned long long capture = 0;  // the capture that took it (graph-owned blocks)
 };
 std::mutex g_scr_mu;
 std::vector<StreamScratch> g_scr;    // eager calls' blocks, one per (device, stream)
@@ -111,17 +112,24 @@ std::vector<StreamScratch> g_scr_g;  // blocks handed to graph captures (owned b
 
 void* stream_scratch(hipStream_t stream, size_t bytes) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) != hipSuccess) return nullptr;
+    unsigned long long cap = 0;
+    if (hipStreamGetCaptureInfo(stream, &cs, &cap) != hipSuccess) return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lock(g_scr_mu);
     if (cs != hipStreamCaptureStatusNone) {
         // a capture cannot allocate: it takes the stream's block from an earlier eager call
         // (the usual warm-up before a capture), which then belongs to the graph -- later eager
-        // calls get a block of their own, so a replay and eager work never share one
+        // calls get a block of their own, so a replay and eager work never share one.  Later
+        // requests of the same capture (the backward after the forward) reuse that block:
+        // they are ordered on the capture stream like the eager calls they replay.
+        if (cs != hipStreamCaptureStatusActive) return nullptr;
+        for (auto& e : g_scr_g)
+            if (e.capture == cap && e.device == dev && e.stream == stream) return e.bytes >= bytes ? e.p : nullptr;
         for (size_t i = 0; i < g_scr.size(); ++i)
             if (g_scr[i].device == dev && g_scr[i].stream == stream && g_scr[i].bytes >= bytes) {
                 g_scr_g.push_back(g_scr[i]);
+                g_scr_g.back().capture = cap;
                 g_scr.erase(g_scr.begin() + (long)i);
                 return g_scr_g.back().p;
             }

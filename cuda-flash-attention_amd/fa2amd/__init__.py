@@ -40,7 +40,7 @@ C_SYMBOLS = (
 # launch-plan overrides fa2_tune_set accepts (include/fa2_amd.h)
 KNOBS = ("FWD_HS", "FWD_WAVES", "FWD_KS", "FWD_NKB", "DKDV_WAVES", "DKDV_QS", "DKDV_HS", "DQ_WAVES", "DQ_KS", "DQ_HS",
          "BWD_FUSED", "BWD_FUSED_DELTA", "BWD_FQS", "BWD_FKS", "BWD_FNW", "HOST_SHARDS_ON_DEVICE0", "HOST_CHUNKS",
-         "FWD_SPLIT")
+         "FWD_SPLIT", "BWD_SPLIT")
 
 
 class FA2Error(RuntimeError):

@@ -1201,7 +1201,7 @@ template <int D>
 __global__ void __launch_bounds__(256, 1)
 fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                      const float* __restrict__ dO, const float* __restrict__ LSE, float* __restrict__ Delta,
-                     float* __restrict__ dQ, int S, const float* __restrict__ O) {
+                     float* __restrict__ dQ, int S, const float* __restrict__ O, int P, float* __restrict__ part) {
     static_assert(D == 64, "hand-scheduled dQ: D = 64");
     constexpr int KT = 64, TB = KT * D, OST = D + 4;
     __shared__ __attribute__((aligned(16))) _Float16 smem[FA2_DQ_LDS_D64 / 2];
@@ -1210,11 +1210,18 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nqb = (S + 255) / 256;
+    // workgroup -> (head, key chunk, query block); P = 1: the whole key range.  P > 1
+    // (the split backward): keys [kc L, kc L + L), the dQ part goes to
+    // part + ((kc BH + bh) S + row) D and chunk 0 writes Δ
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = bid / nqb, qb = bid - bh * nqb;
+    const int qb = bid % nqb, bc = bid / nqb;
+    const int bh = bc / P, kc = bc - bh * P;
     const long base = (long)bh * S * D;
     const long rbase = (long)bh * S;
     const int qrow0 = qb * 256;
+    const int L = S / P;
+    const long kbase = base + (long)kc * L * D;
+    float* dst_rows = P > 1 ? part + ((long)kc * (gridDim.x / (P * nqb)) + bh) * S * D : dQ + base;
 
     // Q block (scaled by log2(e)/sqrt(D)) -> LDS [4TB, 8TB) halves; dO block -> [8TB, 12TB)
     {
@@ -1231,7 +1238,7 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
             TileStager<D, 256, 256> ost;
             ost.init(O + base, S, tid);
             ost.load(qrow0);
-            delta_rows<D, 256, 256>(dst, ost, S, qrow0, rowc[1], Delta + rbase, tid);
+            delta_rows<D, 256, 256>(dst, ost, S, qrow0, rowc[1], kc == 0 ? Delta + rbase : nullptr, tid);
         }
         dst.store(smem + 8 * TB, 1.f, tid);
     }
@@ -1241,8 +1248,8 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
         if (!O) rowc[1][tid] = q < S ? Delta[rbase + q] : 0.f;
     }
     TileStager<D, KT, 256> ks, vs;
-    ks.init(K + base, S, tid);
-    vs.init(V + base, S, tid);
+    ks.init(K + kbase, L, tid);
+    vs.init(V + kbase, L, tid);
     ks.load(0);
     vs.load(0);
     ks.store(smem, 1.f, tid);
@@ -1279,7 +1286,7 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
     const __amdgpu_buffer_rsrc_t hs_rsk = ks.rs, hs_rsv = vs.rs;
     const int hs_qb = __builtin_amdgcn_readfirstlane(4 * TB * 2 + wave * 64 * D * 2);
     const int hs_db = __builtin_amdgcn_readfirstlane(8 * TB * 2 + wave * 64 * D * 2);
-    int hs_cnt = __builtin_amdgcn_readfirstlane(S / KT - 1);
+    int hs_cnt = __builtin_amdgcn_readfirstlane(L / KT - 1);
     int hs_goff = __builtin_amdgcn_readfirstlane(KT * D * 4);
 #ifdef FA2_TILE_BF16
     asm volatile(FA2_DQ_ASM_D64_BF16 : FA2_DQ_OUTPUTS_D64 : FA2_DQ_INPUTS_D64 : FA2_DQ_CLOBBERS_D64);
@@ -1294,7 +1301,7 @@ fa2_bwd_dq_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, c
     for (int rr = 0; rr < 64; rr += RPI) {
         const int row = wave * 64 + rr + lane / LPR, c4 = (lane % LPR) * 4;
         const f32x4 v = *reinterpret_cast<const f32x4*>(os + row * OST + c4) * dscale;
-        if (qrow0 + row < S) *reinterpret_cast<f32x4*>(dQ + base + (long)(qrow0 + row) * D + c4) = v;
+        if (qrow0 + row < S) *reinterpret_cast<f32x4*>(dst_rows + (long)(qrow0 + row) * D + c4) = v;
     }
 }
 // ---------------------------------------------------------------------------
@@ -1320,7 +1327,7 @@ template <int D>
 __global__ void __launch_bounds__(256, 1)
 fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
                        const float* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ Delta,
-                       float* __restrict__ dK, float* __restrict__ dV, int S) {
+                       float* __restrict__ dK, float* __restrict__ dV, int S, int P, float* __restrict__ part) {
     static_assert(D == 64, "hand-scheduled dK/dV: D = 64");
     constexpr int TB = 64 * D, OST = D + 4;
     constexpr int SLOT = FA2_DK_SLOT_D64, RC = FA2_DK_RC_D64, KVB = FA2_DK_KVB_D64;
@@ -1330,11 +1337,19 @@ fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K,
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nkb = (S + 255) / 256;
+    // workgroup -> (head, query chunk, key block); P = 1: every query.  P > 1 (the split
+    // backward): queries [qc L, qc L + L), the dK / dV parts go to
+    // part + ((qc BH + bh) S + row) D and part + (P BH + qc BH + bh) S D + row D
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = bid / nkb, kblk = bid - bh * nkb;
+    const int kblk = bid % nkb, bc = bid / nkb;
+    const int bh = bc / P, qc = bc - bh * P;
     const long base = (long)bh * S * D;
     const long rbase = (long)bh * S;
     const int krow0 = kblk * 256;
+    const int L = S / P, q0 = qc * L;
+    const long BH = gridDim.x / (P * nkb);
+    float* dk_rows = P > 1 ? part + ((long)qc * BH + bh) * S * D : dK + base;
+    float* dv_rows = P > 1 ? part + ((long)P * BH + (long)qc * BH + bh) * S * D : dV + base;
 
     // K block (scaled) and V block -> LDS [KVB, KVB + 2 * 256 * D * 2) bytes
     {
@@ -1351,16 +1366,16 @@ fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K,
     }
     // step 0: Q, dO tiles and the row constants -> slot 0
     TileStager<D, 64, 256> qs, ds;
-    qs.init(Q + base, S, tid);
-    ds.init(dO + base, S, tid);
+    qs.init(Q + base + (long)q0 * D, L, tid);
+    ds.init(dO + base + (long)q0 * D, L, tid);
     qs.load(0);
     ds.load(0);
     qs.store(sh, 1.f, tid);
     ds.store(sh + TB, 1.f, tid);
     if (tid < 64) {
         float* rc = reinterpret_cast<float*>(lds + RC);
-        rc[tid] = tid < S ? -LSE[rbase + tid] * FA2B_LOG2E : 0.f;
-        rc[64 + tid] = tid < S ? -Delta[rbase + tid] : 0.f;
+        rc[tid] = tid < L ? -LSE[rbase + q0 + tid] * FA2B_LOG2E : 0.f;
+        rc[64 + tid] = tid < L ? -Delta[rbase + q0 + tid] : 0.f;
     }
     __syncthreads();
 
@@ -1386,11 +1401,12 @@ fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K,
     const int hs_oak = ((wave * 64 + i16) * OST + 4 * g16) * 4, hs_oav = hs_oak + 256 * OST * 4;
     const __amdgpu_buffer_rsrc_t hs_rsq = qs.rs, hs_rsd = ds.rs;
     // the row-constant stream of this wave: LSE (wave 0), Δ (wave 1), nothing (num_records 0)
-    const __amdgpu_buffer_rsrc_t hs_rsc = head_rsrc(wave == 1 ? Delta + rbase : LSE + rbase, wave < 2 ? S : 0, 1);
+    const __amdgpu_buffer_rsrc_t hs_rsc =
+        head_rsrc(wave == 1 ? Delta + rbase + q0 : LSE + rbase + q0, wave < 2 ? L : 0, 1);
     const float hs_rsm = __builtin_bit_cast(
         float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, wave == 0 ? -FA2B_LOG2E : wave == 1 ? -1.f : 0.f)));
     const int hs_kvb = __builtin_amdgcn_readfirstlane(KVB + wave * 64 * D * 2);
-    int hs_cnt = __builtin_amdgcn_readfirstlane(S / 64 - 1);
+    int hs_cnt = __builtin_amdgcn_readfirstlane(L / 64 - 1);
     int hs_goff = __builtin_amdgcn_readfirstlane(64 * D * 4);
     int hs_roff = __builtin_amdgcn_readfirstlane(64 * 4);
     (void)SLOT;
@@ -1409,10 +1425,25 @@ fa2_bwd_dkdv_hs_kernel(const float* __restrict__ Q, const float* __restrict__ K,
         const f32x4 vk = *reinterpret_cast<const f32x4*>(os + row * OST + c4) * dscale;
         const f32x4 vv = *reinterpret_cast<const f32x4*>(os + (256 + row) * OST + c4);
         if (krow0 + row < S) {
-            *reinterpret_cast<f32x4*>(dK + base + (long)(krow0 + row) * D + c4) = vk;
-            *reinterpret_cast<f32x4*>(dV + base + (long)(krow0 + row) * D + c4) = vv;
+            *reinterpret_cast<f32x4*>(dk_rows + (long)(krow0 + row) * D + c4) = vk;
+            *reinterpret_cast<f32x4*>(dv_rows + (long)(krow0 + row) * D + c4) = vv;
         }
     }
+}
+
+// The split backward's reduce: out[t] = sum over the P chunk parts of tensor t (dQ, dK,
+// dV; blockIdx.y), in chunk order -- deterministic.  n floats per tensor, 4 per thread.
+__global__ void __launch_bounds__(256)
+fa2_bwd_split_reduce_kernel(const float* __restrict__ part, int P, long n, float* __restrict__ dq,
+                            float* __restrict__ dk, float* __restrict__ dv) {
+    const long x = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (x >= n) return;
+    const int t = blockIdx.y;
+    const float* src = part + (long)t * P * n + x;
+    f32x4 acc = *reinterpret_cast<const f32x4*>(src);
+    for (int c = 1; c < P; ++c) acc += *reinterpret_cast<const f32x4*>(src + c * n);
+    float* out = t == 0 ? dq : t == 1 ? dk : dv;
+    *reinterpret_cast<f32x4*>(out + x) = acc;
 }
 #endif  // CUPY_INLINE_COMPILE
 
@@ -1715,7 +1746,7 @@ hipError_t dkdv_dispatch(const float* q, const float* k, const float* v, const f
         if (fits && (hs == 1 || (hs < 0 && nw == 0 && qs == 0 && hgrid >= cu_count()))) {
             if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
             hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_hs_kernel<D>), dim3((unsigned)hgrid), dim3(256), 0, stream, q, k,
-                               v, dout, lse, delta, dk, dv, S);
+                               v, dout, lse, delta, dk, dv, S, 1, nullptr);
             return hipGetLastError();
         }
     }
@@ -1781,7 +1812,7 @@ hipError_t dq_dispatch(const float* q, const float* k, const float* v, const flo
         if (fits && (hs == 1 || (hs < 0 && nw == 0 && ksp == 0 && hgrid >= cu_count()))) {
             if (hgrid > 0x7fffffffL) return hipErrorInvalidValue;
             hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<D>), dim3((unsigned)hgrid), dim3(256), 0, stream, q, k, v,
-                               dout, lse, delta, dq, S, o);
+                               dout, lse, delta, dq, S, o, 1, nullptr);
             return hipGetLastError();
         }
     }
@@ -1938,6 +1969,56 @@ hipError_t launch_bwd_fused_delta(int D, const float* q, const float* k, const f
 }
 }  // namespace
 
+// The split backward (D = 64, grids below one 256-row workgroup per CU): the
+// hand-scheduled dQ kernel on P key chunks (Δ fused, written by chunk 0), the
+// hand-scheduled dK/dV kernel on P query chunks, both leaving fp32 parts in the stream's
+// scratch block, then one ordered reduce of the three tensors.  BWD_SPLIT (tests and
+// tools): P >= 2 forces it (an error where it cannot serve: D, shape, other backward plan
+// knobs, or no scratch -- a stream being captured without an earlier eager block),
+// 1 disables it, 0 = auto (bwd_split_auto).  hipErrorNotSupported: not this plan.
+// Chunks per head for a grid of `g` 256-row blocks: only where the unsplit plans leave
+// most CUs idle with long heads (g <= 64 at S >= 4096, g <= 16 at S >= 2048), the most
+// chunks (a power of two, at most 8) that keep one workgroup per CU and chunks of at
+// least 256 rows.  r06 in-process A/B of fa2_backward (profiles/r06/bsplit/), the
+// small-grid plan -> split: B1_H2_S4096 88.2 -> 59.6 us (P = 8), B1_H4_S4096 92.9 -> 87.9
+// (4), B1_H2_S8192 177.9 -> 149.7 (4), B1_H2_S2048 42.9 -> 37.4 (8); B1_H4_S2048 ties,
+// B1_H8_S4096 / B1_H8_S2048 / B2_H8_S2048 lose 1-40 % (three fp32 part tensors and the
+// reduce grow with the workgroups; the fused small-grid plan does no recompute).
+static int bwd_split_auto(long g, int S) {
+    if (!(S >= 4096 && g <= 64) && !(S >= 2048 && g <= 16)) return 1;
+    const long ncu = cu_count();
+    int P = 1;
+    while (P < 8 && g * (2 * P) <= ncu && S % (64 * 2 * P) == 0 && S / (2 * P) >= 256) P *= 2;
+    return P;
+}
+static hipError_t bwd_split_plan(int D, const float* q, const float* k, const float* v, const float* o, const float* dout,
+                          const float* lse, float* delta, float* dq, float* dk, float* dv, int bh, int S,
+                          hipStream_t stream) {
+    const int split = tune_knob("BWD_SPLIT", 0);
+    if (split < 0) return hipErrorInvalidValue;
+    if (split == 1) return hipErrorNotSupported;
+    const bool fits = D == 64 && bh > 0 && S % 64 == 0 && S >= 128;
+    const bool forced_other = tune_knob("BWD_FUSED", -1) >= 0 || tune_knob("DQ_HS", -1) >= 0 ||
+                              tune_knob("DKDV_HS", -1) >= 0 || tune_knob("DQ_WAVES", 0) || tune_knob("DQ_KS", 0) ||
+                              tune_knob("DKDV_WAVES", 0) || tune_knob("DKDV_QS", 0);
+    if (split >= 2 && (!fits || forced_other || S % (64 * split) || S / split < 128)) return hipErrorInvalidValue;
+    const long g = fits ? (long)bh * ((S + 255) / 256) : 0;
+    const int P = split >= 2 ? split : (fits && !forced_other && g < cu_count()) ? bwd_split_auto(g, S) : 1;
+    if (P < 2) return hipErrorNotSupported;
+    const long n = (long)bh * S * D;
+    float* part = static_cast<float*>(stream_scratch(stream, sizeof(float) * 3 * P * (size_t)n));
+    if (!part) return split >= 2 ? hipErrorInvalidValue : hipErrorNotSupported;
+    const long grid = g * P;
+    if (grid > 0x7fffffffL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dq_hs_kernel<64>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v, dout,
+                       lse, delta, dq, S, o, P, part);
+    hipLaunchKernelGGL((fa2f16b::fa2_bwd_dkdv_hs_kernel<64>), dim3((unsigned)grid), dim3(256), 0, stream, q, k, v,
+                       dout, lse, delta, dk, dv, S, P, part + (long)P * n);
+    hipLaunchKernelGGL(fa2f16b::fa2_bwd_split_reduce_kernel, dim3((unsigned)((n / 4 + 255) / 256), 3), dim3(256), 0,
+                       stream, part, P, n, dq, dk, dv);
+    return hipGetLastError();
+}
+
 // Override BWD_FUSED (fa2_tune_set): 1 = Δ kernel, then dK/dV and dQ in one launch (D <= 64);
 // 0 = Δ fused into the dQ kernel's prologue (which stages dO anyway), then dK/dV,
 // which reads it; -1 (default) = 1 on grids of fewer than 8 blocks of 32 rows per
@@ -1946,6 +2027,10 @@ hipError_t launch_bwd_fused_delta(int D, const float* q, const float* k, const f
 hipError_t FA2_TILE_LAUNCH(launch_backward)(int D, const float* q, const float* k, const float* v, const float* o,
                                const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv,
                                int bh, int S, hipStream_t stream) {
+    {
+        const hipError_t e = bwd_split_plan(D, q, k, v, o, dout, lse, delta, dq, dk, dv, bh, S, stream);
+        if (e != hipErrorNotSupported) return e;
+    }
     int fused = tune_knob("BWD_FUSED", -1);
     if (fused < 0) fused = bh > 0 && S > 0 && auto_waves((long)bh * ((S + 31) / 32), 8) < 8;
     if (D <= 64 && bh > 0 && S > 0 && fused == 1) {
