@@ -129,7 +129,7 @@ int fa2_shard_range(int total_heads, int shards, int index, int* first, int* cou
 /* Launch-plan override (tests and tuning tools only; nothing is read from the
  * environment).  fa2_tune_set("DKDV_QS", 2) makes the next launches use that plan
  * where the shape allows it; fa2_tune_set(NULL, 0) clears every override.  Knobs:
- * FWD_HS, FWD_SPLIT, FWD_WAVES, FWD_KS, FWD_NKB, DKDV_HS, DKDV_WAVES, DKDV_QS, DQ_HS, DQ_WAVES,
+ * FWD_HS, FWD_SPLIT, FWD_WAVES, FWD_KS, FWD_NKB, BWD_SPLIT, DKDV_HS, DKDV_WAVES, DKDV_QS, DQ_HS, DQ_WAVES,
  * DQ_KS, BWD_FUSED, BWD_FUSED_DELTA, BWD_FQS, BWD_FKS, BWD_FNW (see the launchers in
  * kernels/; a value that forces a plan the shape cannot take is FA2_E_INVALID at the
  * launch, never a silent fallback), and
