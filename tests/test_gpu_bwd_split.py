@@ -197,3 +197,36 @@ def test_split_step_graph_capture():
         torch.cuda.synchronize()
         for name, a, b in zip(("o", "lse", "dq", "dk", "dv"), eager, (o, lse, dq, dk, dv)):
             assert torch.equal(a, b), name
+
+
+def test_split_plans_on_two_streams_at_once():
+    """two streams run split forward + backward steps concurrently: each stream has its own
+    scratch block, so both give bitwise what a lone step gives"""
+    fa2amd.tune_set("FWD_SPLIT", 4)
+    fa2amd.tune_set("BWD_SPLIT", 4)
+    cases = []
+    for seed in (31, 32):
+        (q, k, v, do, _, _), _ = _case((1, 2, 2048, 64), seed=seed)
+        tq, tk, tv, tdo = cuda(q, k, v, do)
+        cases.append((tq, tk, tv, tdo))
+
+    def step(tq, tk, tv, tdo):
+        o, lse = fa2amd.forward(tq, tk, tv, "fp16")
+        return (o, lse) + tuple(fa2amd.backward(tq, tk, tv, o, tdo, lse, "fp16"))
+
+    alone = []
+    for c in cases:
+        alone.append([t.clone() for t in step(*c)])
+        torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream())
+    outs = [None, None]
+    for _ in range(3):
+        for i, (s, c) in enumerate(zip(streams, cases)):
+            with torch.cuda.stream(s):
+                outs[i] = step(*c)
+        torch.cuda.synchronize()
+        for a, b in zip(alone, outs):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y)
