@@ -1133,8 +1133,11 @@ static hipError_t fwd_hs_launch(const float* q, const float* k, const float* v, 
 //            B2_H8_S2048 66.9 -> 51.1 (2), B1_H8_S4096 124.7 -> 78.2 (2), B2_H8_S1024
 //            33.8 -> 30.8 (4); S = 512 loses (19.0 -> 20.9).
 static int fwd_split_auto(int D, long g, int S) {
-    const int min_s = D == 128 ? 1024 : 4096, min_chunk = D == 128 ? 256 : 1024;
-    if (S < min_s) return 1;
+    // D = 64 also at S >= 2048 on grids of <= 16 blocks (2 heads): 20.1 -> 17.9 us at
+    // B1_H2_S2048 (P = 4), where the split backward runs too (§6 of DESIGN.md)
+    const bool tiny = D == 64 && S >= 2048 && g <= 16;
+    const int min_s = D == 128 ? 1024 : 4096, min_chunk = D == 128 ? 256 : tiny ? 512 : 1024;
+    if (S < min_s && !tiny) return 1;
     const long ncu = cu_count();
     int P = 1;
     while (P < 4 && g * (2 * P) <= ncu && S % (64 * 2 * P) == 0 && S / (2 * P) >= min_chunk) P *= 2;

@@ -59,8 +59,9 @@ def auto_split(bh, S, D):
     """the library's rule (kernel_fa2_optimized_f16.cu, fwd_split_auto)"""
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
     g = bh * ((S + 255) // 256)
-    min_s, min_chunk = (1024, 256) if D == 128 else (4096, 1024)
-    if g >= ncu or S % 64 or S < min_s:
+    tiny = D == 64 and S >= 2048 and g <= 16
+    min_s, min_chunk = (1024, 256) if D == 128 else (4096, 512 if tiny else 1024)
+    if g >= ncu or S % 64 or (S < min_s and not tiny):
         return 1
     P = 1
     while P < 4 and g * 2 * P <= ncu and S % (128 * P) == 0 and S // (2 * P) >= min_chunk:
@@ -140,7 +141,8 @@ def test_split_matches_unsplit():
     assert maxerr(l1, l0) < 2e-3
 
 
-@pytest.mark.parametrize("shape", [(1, 2, 4096, 64), (1, 8, 4096, 64), (1, 4, 2048, 64), (2, 8, 1024, 64),
+@pytest.mark.parametrize("shape", [(1, 2, 4096, 64), (1, 8, 4096, 64), (1, 2, 2048, 64), (1, 4, 2048, 64),
+                                   (2, 8, 1024, 64),
                                    (1, 2, 2048, 128), (2, 8, 1024, 128), (2, 8, 512, 128)])
 def test_split_auto_rule(shape):
     """below a full grid the default plan is the split with fwd_split_auto's chunk count
